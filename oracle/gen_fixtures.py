@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""oracle/gen_fixtures.py -- TEST INFRASTRUCTURE ONLY: (re)generates tests/golden/.
+
+Runs in the build container only (needs /root/reference and oracle/_ref/, built by
+`make -C oracle ref`).  Everything written under tests/golden/ is DATA: inputs and expected
+outputs.  Nothing written here is reference source text.
+
+  tests/golden/inputs/<test>/core_<n>.txt      the reference's own test inputs (data files,
+                                               /root/reference/tests/<test>/core_<n>.txt)
+  tests/golden/lockstep/<test>/core_<n>_output.txt
+                                               printProcessorState dumps produced by the
+                                               reference's handler text driven under the
+                                               lock-step schedule (oracle/_ref/ref_lockstep_np4_i32)
+  tests/golden/lockstep/summary.json           per test: status, rounds, msgs, instrs, hashes,
+                                               md5 of every dump
+  tests/golden/observed/<test>.json            outcome sets of the UNMODIFIED reference binary
+                                               (oracle/_ref/cache_simulator_ref, OpenMP,
+                                               nondeterministic, never exits -> run under
+                                               `timeout`), RUNS runs per test
+  tests/golden/ensemble/<name>.npy             per-system results [n, 6] uint64 (status,
+                                               rounds, msgs, instrs, dump_hash, final_hash)
+                                               from oracle/_ref/ref_lockstep_np{4,8} over the
+                                               counter-based generator
+  tests/golden/ensemble/<name>_recs.npy        first 16 systems' dump + final node records
+                                               uint8 [16, 2, np, 64]
+  tests/golden/ensemble/meta.json              generator parameters per fixture
+"""
+import concurrent.futures as cf
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = os.environ.get("REF", "/root/reference")
+REFBIN = os.path.join(HERE, "_ref")
+GOLD = os.path.join(REPO, "tests", "golden")
+TESTS = ["sample", "test_1", "test_2", "test_3", "test_4"]
+RUNS = int(os.environ.get("RUNS", "200"))
+
+ENSEMBLES = [  # name, np, dist, seed, n_instr, first_sys, n_sys
+    ("np8_uniform", 8, 0, 1, 4096, 0, 4096),
+    ("np8_hot", 8, 1, 1, 4096, 0, 2048),
+    ("np8_evict", 8, 2, 1, 4096, 0, 4096),
+    ("np4_uniform", 4, 0, 1, 4096, 0, 4096),
+    ("np8_uniform_far", 8, 0, 1, 4096, 999_000, 1024),  # ids near the end of the 1M bench set
+]
+RES_DT = np.dtype([("status", "<u4"), ("rounds", "<u4"), ("msgs", "<u4"), ("instrs", "<u4"),
+                   ("dump_hash", "<u8"), ("final_hash", "<u8")])
+
+
+def md5(b):
+    return hashlib.md5(b).hexdigest()
+
+
+def res_to_u64(r):
+    return np.stack([r["status"].astype(np.uint64), r["rounds"].astype(np.uint64),
+                     r["msgs"].astype(np.uint64), r["instrs"].astype(np.uint64),
+                     r["dump_hash"], r["final_hash"]], axis=1)
+
+
+def read_ref_bin(path, np_):
+    rec = 32 + 2 * np_ * 64
+    b = np.fromfile(path, dtype=np.uint8).reshape(-1, rec)
+    res = b[:, :32].copy().view(RES_DT).reshape(-1)
+    recs = b[:, 32:].reshape(-1, 2, np_, 64)
+    return res, recs
+
+
+def inputs():
+    for t in TESTS:
+        d = os.path.join(GOLD, "inputs", t)
+        os.makedirs(d, exist_ok=True)
+        for n in range(4):
+            shutil.copyfile(os.path.join(REF, "tests", t, f"core_{n}.txt"),
+                            os.path.join(d, f"core_{n}.txt"))
+
+
+def lockstep():
+    summary = {}
+    for t in TESTS:
+        with tempfile.TemporaryDirectory() as tmp:
+            os.symlink(os.path.join(GOLD, "inputs"), os.path.join(tmp, "tests"))
+            subprocess.run([os.path.join(REFBIN, "ref_lockstep_np4_i32"), "tests", t, "res.bin"],
+                           cwd=tmp, check=True, stdout=subprocess.DEVNULL)
+            res, recs = read_ref_bin(os.path.join(tmp, "res.bin"), 4)
+            d = os.path.join(GOLD, "lockstep", t)
+            os.makedirs(d, exist_ok=True)
+            md5s = {}
+            for n in range(4):
+                src = os.path.join(tmp, f"core_{n}_output.txt")
+                if os.path.exists(src):
+                    shutil.copyfile(src, os.path.join(d, f"core_{n}_output.txt"))
+                    md5s[n] = md5(open(src, "rb").read())
+            r = res[0]
+            summary[t] = dict(status=int(r["status"]) & 0xFF, dumped_mask=int(r["status"]) >> 8,
+                              rounds=int(r["rounds"]), msgs=int(r["msgs"]),
+                              instrs=int(r["instrs"]), dump_hash=int(r["dump_hash"]),
+                              final_hash=int(r["final_hash"]), md5=md5s)
+            np.save(os.path.join(d, "records.npy"), recs[0])
+    with open(os.path.join(GOLD, "lockstep", "summary.json"), "w") as f:
+        json.dump(summary, f, indent=1, sort_keys=True)
+
+
+def one_run(t):
+    with tempfile.TemporaryDirectory() as tmp:
+        os.symlink(os.path.join(GOLD, "inputs"), os.path.join(tmp, "tests"))
+        subprocess.run(["timeout", "0.3", os.path.join(REFBIN, "cache_simulator_ref"), t],
+                       cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        out = {}
+        for n in range(4):
+            p = os.path.join(tmp, f"core_{n}_output.txt")
+            out[n] = open(p, "rb").read() if os.path.exists(p) else None
+        return out
+
+
+def observed():
+    os.makedirs(os.path.join(GOLD, "observed"), exist_ok=True)
+    with cf.ThreadPoolExecutor(8) as ex:
+        for t in TESTS:
+            runs = list(ex.map(one_run, [t] * RUNS))
+            cores = {}
+            for n in range(4):
+                outs, missing = {}, 0
+                for r in runs:
+                    b = r[n]
+                    if b is None or len(b) == 0:
+                        missing += 1
+                        continue
+                    h = md5(b)
+                    e = outs.setdefault(h, {"count": 0, "text": b.decode()})
+                    e["count"] += 1
+                cores[str(n)] = {"missing": missing, "outcomes": outs}
+            with open(os.path.join(GOLD, "observed", f"{t}.json"), "w") as f:
+                json.dump({"runs": RUNS, "binary": "assignment.c, gcc -O2 -fopenmp, timeout 0.3 s",
+                           "cores": cores}, f, indent=1, sort_keys=True)
+
+
+def ensemble():
+    d = os.path.join(GOLD, "ensemble")
+    os.makedirs(d, exist_ok=True)
+    meta = {}
+    for name, np_, dist, seed, n_instr, first, n in ENSEMBLES:
+        with tempfile.TemporaryDirectory() as tmp:
+            out = os.path.join(tmp, "e.bin")
+            subprocess.run([os.path.join(REFBIN, f"ref_lockstep_np{np_}"), "gen", str(dist),
+                            str(seed), str(n_instr), str(first), str(n), out], check=True)
+            res, recs = read_ref_bin(out, np_)
+        np.save(os.path.join(d, f"{name}.npy"), res_to_u64(res))
+        np.save(os.path.join(d, f"{name}_recs.npy"), np.ascontiguousarray(recs[:16]))
+        meta[name] = dict(np=np_, dist=dist, seed=seed, n_instr=n_instr, first_sys=first, n_sys=n)
+    with open(os.path.join(d, "meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    if not os.path.exists(os.path.join(REF, "assignment.c")) or \
+            not os.path.exists(os.path.join(REFBIN, "ref_lockstep_np8")):
+        sys.exit("gen_fixtures: needs /root/reference and oracle/_ref (make -C oracle ref)")
+    steps = sys.argv[1:] or ["inputs", "lockstep", "observed", "ensemble"]
+    for s in steps:
+        print("gen_fixtures:", s, flush=True)
+        globals()[s]()

@@ -1,0 +1,265 @@
+/*
+ * oracle/ref_lockstep.c -- TEST INFRASTRUCTURE ONLY.  Built into oracle/_ref/ by
+ * oracle/build_ref.sh when /root/reference is present; never shipped, never linked into
+ * the product.
+ *
+ * Drives the reference's OWN code (/root/reference/assignment.c) single-threaded under the
+ * deterministic lock-step schedule.  build_ref.sh extracts these line
+ * ranges into a scratch directory at build time (they never enter this repository):
+ *   frag_types.inc    assignment.c:15-81   types (NUM_PROCS / MAX_INSTR_NUM given by -D)
+ *   frag_helpers.inc  assignment.c:94-115  isBitSet / findOwner / countSharers
+ *   frag_handler.inc  assignment.c:177-566 message decode + 13-way handler switch
+ *   frag_issue.inc    assignment.c:590-697 instruction issue + dump-once block
+ *   frag_repl.inc     assignment.c:742-773 handleCacheReplacement
+ *   frag_init.inc     assignment.c:776-822 initializeProcessor
+ *   frag_print.inc    assignment.c:824-876 printProcessorState
+ * This file supplies only what replaces the OpenMP runtime: per-node contexts for the loop
+ * locals of main (:137-146), a staging sendMessage (deliveries at the end of each round,
+ * ascending sender then program order), the round loop, and a record/hash writer.
+ *
+ * Usage:
+ *   ref_lockstep tests <name> <out.bin>      (CWD must contain tests/<name>/core_n.txt;
+ *                                            dumps written to CWD by printProcessorState)
+ *   ref_lockstep gen <dist> <seed> <n_instr> <first_sys> <n_sys> <out.bin>
+ * out.bin: per system one dsm_res, then NUM_PROCS dump records, then NUM_PROCS final records.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+#include <ctype.h>
+#include <sys/stat.h>
+#include <stdint.h>
+#include "dsm_common.h"
+
+#ifndef NUM_PROCS
+#error "NUM_PROCS must be given"
+#endif
+#define CACHE_SIZE 4
+#define MEM_SIZE 16
+#define MSG_BUFFER_SIZE 256
+
+/* asserts of the regular build abort the process; here they end the system with
+ * ST_ASSERT_FAILED (the enclosing handler returns at the failed assert). */
+static int g_assert_failed;
+#define assert(e) do { if (!(e)) { g_assert_failed = 1; return; } } while (0)
+
+#include "frag_types.inc"
+
+void initializeProcessor(int threadId, processorNode *node, char *dirName);
+void sendMessage(int receiver, message msg);
+void handleCacheReplacement(int sender, cacheLine oldCacheLine);
+void printProcessorState(int processorId, processorNode node);
+
+#include "frag_helpers.inc"
+
+#define MAX_STAGED 1024
+static message st_msg[MAX_STAGED];
+static int st_dest[MAX_STAGED];
+static int nst;
+
+void sendMessage(int receiver, message msg) {
+    if (nst < MAX_STAGED) { st_dest[nst] = receiver; st_msg[nst] = msg; }
+    nst++;
+}
+
+#include "frag_repl.inc"
+#include "frag_init.inc"
+#include "frag_print.inc"
+
+typedef struct {
+    processorNode node;
+    message msgReply;
+    instruction instr;
+    int instructionIdx;
+    int instructions_done;
+    processorNode dumpSnap;
+    int dumped;
+    message ring[MSG_BUFFER_SIZE];
+    int head, count;
+} nodeCtx;
+
+static nodeCtx C[NUM_PROCS];
+static int g_write_files;
+
+static void capture_dump(int id, processorNode n) {
+    C[id].dumpSnap = n;
+    C[id].dumped = 1;
+    if (g_write_files) printProcessorState(id, n);
+}
+
+static void handle(int threadId, nodeCtx *c, message msg) {
+#define node (c->node)
+#define msgReply (c->msgReply)
+#include "frag_handler.inc"
+#undef node
+#undef msgReply
+}
+
+static void issue(int threadId, nodeCtx *c) {
+#define node (c->node)
+#define instr (c->instr)
+#define instructionIdx (c->instructionIdx)
+#define instructions_done (c->instructions_done)
+#define printProcessorState capture_dump
+#include "frag_issue.inc"
+#undef printProcessorState
+#undef instructions_done
+#undef instructionIdx
+#undef instr
+#undef node
+}
+
+static void to_rec(const processorNode *n, int waiting, int done, int issued, dsm_rec *r) {
+    memset(r, 0, sizeof *r);
+    for (int i = 0; i < 16; ++i) {
+        r->memory[i] = n->memory[i];
+        r->dir_bv[i] = n->directory[i].bitVector;
+        r->dir_state[i] = (uint8_t)n->directory[i].state;
+    }
+    for (int i = 0; i < 4; ++i) {
+        r->cache_addr[i] = n->cache[i].address;
+        r->cache_value[i] = n->cache[i].value;
+        r->cache_state[i] = (uint8_t)n->cache[i].state;
+    }
+    r->pending = n->pendingWriteValue;
+    r->flags = (uint8_t)((waiting ? 1 : 0) | (done ? 2 : 0));
+    r->issued = (uint16_t)issued;
+}
+
+/* main :137-146 locals, then the lock-step schedule in place of :153-699 */
+static void reset_ctx(int t) {
+    memset(&C[t], 0, sizeof C[t]);
+    C[t].instructionIdx = -1;
+    C[t].instructions_done = 0;
+    C[t].node.waitingForReply = 0;
+    C[t].node.pendingWriteValue = 0;
+    C[t].node.outstandingMsgs = 0;
+}
+
+static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
+    uint32_t rounds = 0, msgs = 0, instrs = 0, status = ST_COMPLETED;
+    g_assert_failed = 0;
+    for (uint32_t r = 1;; ++r) {
+        int acted = 0;
+        nst = 0;
+        for (int t = 0; t < NUM_PROCS; ++t) {
+            nodeCtx *c = &C[t];
+            if (c->count > 0) {
+                message m = c->ring[c->head];
+                c->head = (c->head + 1) % MSG_BUFFER_SIZE;
+                c->count--;
+                handle(t, c, m);
+                acted = 1; msgs++;
+            } else if (c->node.waitingForReply > 0) {
+            } else if (!c->instructions_done) {
+                int before = c->instructionIdx;
+                issue(t, c);
+                if (c->instructionIdx != before) instrs++;
+                acted = 1;
+            }
+            if (g_assert_failed) break;
+        }
+        if (g_assert_failed) { status = ST_ASSERT_FAILED; rounds = r; break; }
+        int ovf = (nst > MAX_STAGED);
+        for (int k = 0; k < nst && !ovf; ++k) {
+            nodeCtx *d = &C[st_dest[k]];
+            if (d->count >= MSG_BUFFER_SIZE) { ovf = 1; break; }
+            d->ring[(d->head + d->count) % MSG_BUFFER_SIZE] = st_msg[k];
+            d->count++;
+        }
+        if (ovf) { status = ST_RING_OVERFLOW; rounds = r; break; }
+        if (!acted) {
+            int all = 1;
+            for (int t = 0; t < NUM_PROCS; ++t) all &= C[t].dumped;
+            status = all ? ST_COMPLETED : ST_DEADLOCKED;
+            break;
+        }
+        rounds = r;
+        if (r >= DSM_ROUND_LIMIT) { status = ST_ROUND_LIMIT; break; }
+    }
+    uint32_t mask = 0;
+    uint64_t dh = 0, fh = 0;
+    for (int t = 0; t < NUM_PROCS; ++t) {
+        memset(&dump[t], 0, sizeof dump[t]);
+        if (C[t].dumped) {
+            mask |= 1u << t;
+            to_rec(&C[t].dumpSnap, C[t].dumpSnap.waitingForReply, 1,
+                   C[t].instructionIdx + 1, &dump[t]);
+            dh += dsm_hash_rec(t, &dump[t], DSM_DUMP_WORDS);
+        }
+        to_rec(&C[t].node, C[t].node.waitingForReply, C[t].instructions_done,
+               C[t].instructionIdx + 1, &fin[t]);
+        fh += dsm_hash_rec(t, &fin[t], DSM_FINAL_WORDS);
+    }
+    res->status = status | (mask << 8);
+    res->rounds = rounds; res->msgs = msgs; res->instrs = instrs;
+    res->dump_hash = dh; res->final_hash = fh;
+}
+
+static void write_sys(FILE *f, const dsm_res *res, const dsm_rec *dump, const dsm_rec *fin) {
+    fwrite(res, sizeof *res, 1, f);
+    fwrite(dump, sizeof(dsm_rec), NUM_PROCS, f);
+    fwrite(fin, sizeof(dsm_rec), NUM_PROCS, f);
+}
+
+int main(int argc, char **argv) {
+    dsm_res res;
+    dsm_rec dump[NUM_PROCS], fin[NUM_PROCS];
+    if (argc == 4 && !strcmp(argv[1], "tests")) {
+        FILE *f = fopen(argv[3], "wb");
+        if (!f) { perror("open out"); return 1; }
+        g_write_files = 1;
+        for (int t = 0; t < NUM_PROCS; ++t) {
+            reset_ctx(t);
+            initializeProcessor(t, &C[t].node, argv[2]);
+        }
+        fflush(stdout);
+        run_system(&res, dump, fin);
+        write_sys(f, &res, dump, fin);
+        fclose(f);
+        return 0;
+    }
+    if (argc == 8 && !strcmp(argv[1], "gen")) {
+        int dist = atoi(argv[2]);
+        uint64_t seed = strtoull(argv[3], 0, 0);
+        int n_instr = atoi(argv[4]);
+        uint64_t first = strtoull(argv[5], 0, 0), n = strtoull(argv[6], 0, 0);
+        if (n_instr > MAX_INSTR_NUM) { fprintf(stderr, "n_instr > MAX_INSTR_NUM\n"); return 1; }
+        FILE *f = fopen(argv[7], "wb");
+        if (!f) { perror("open out"); return 1; }
+        /* initializeProcessor reads tests/<dir>/core_n.txt: give it empty files in a
+         * scratch CWD, then install the generated instructions (:802-818 layout). */
+        char tmpl[] = "/tmp/reflsXXXXXX";
+        if (!mkdtemp(tmpl) || chdir(tmpl)) { perror("scratch"); return 1; }
+        mkdir("tests", 0700); mkdir("tests/empty", 0700);
+        for (int t = 0; t < NUM_PROCS; ++t) {
+            char p[64]; snprintf(p, sizeof p, "tests/empty/core_%d.txt", t);
+            FILE *e = fopen(p, "w"); if (e) fclose(e);
+        }
+        if (!freopen("/dev/null", "w", stdout)) return 1;
+        for (uint64_t s = 0; s < n; ++s) {
+            for (int t = 0; t < NUM_PROCS; ++t) {
+                reset_ctx(t);
+                initializeProcessor(t, &C[t].node, "empty");
+                for (int i = 0; i < n_instr; ++i) {
+                    uint16_t w = dsm_gen_instr(seed, dist, NUM_PROCS, first + s, t, (uint32_t)i);
+                    C[t].node.instructions[i].type = (w >> 15) ? 'W' : 'R';
+                    C[t].node.instructions[i].address = (byte)((w >> 8) & 0x7F);
+                    C[t].node.instructions[i].value = (byte)(w & 0xFF);
+                }
+                C[t].node.instructionCount = n_instr;
+            }
+            run_system(&res, dump, fin);
+            write_sys(f, &res, dump, fin);
+        }
+        fclose(f);
+        for (int t = 0; t < NUM_PROCS; ++t) {
+            char p[64]; snprintf(p, sizeof p, "tests/empty/core_%d.txt", t); unlink(p);
+        }
+        rmdir("tests/empty"); rmdir("tests"); if (chdir("/")) {} rmdir(tmpl);
+        return 0;
+    }
+    fprintf(stderr, "usage: %s tests <name> <out.bin> | gen <dist> <seed> <n_instr> <first> <n> <out.bin>\n", argv[0]);
+    return 2;
+}
