@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""bench.py -- simulated coherence transactions/sec (whole node) + % HBM roofline.
+
+A "step" is one pass of the hot path (lock-step transition kernel + 256-deep re-run of
+overflowing systems + counter reduction) over this rank's batch of synthetic systems, whose
+packed traces are already resident in HBM (generated on the device before warmup; the
+generator pass is timed separately as the trace-streaming phase).
+
+Default workload (N=1): BASELINE.json configs[2] / SURVEY 8d C3 -- 1M synthetic 8-node
+systems, uniform RD/WR over 0x00-0x7F, 4096 instructions per node, seed 1.  With N GPUs each
+rank simulates its own 1M systems (ids rank*1M ..), i.e. weak scaling; the only collective is
+the final RCCL all-reduce of the counters.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config random|hot|evict]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "hp-assignment-2_amd")
+ORACLE = os.path.join(REPO, "oracle")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "simulated coherence transactions/sec (whole node) + % HBM roofline, 1/2/4/8 GPU"
+UNIT = "transactions/s"
+
+CONFIGS = {
+    # name: (dist, systems per GPU, instructions per node, seed, workload description)
+    "random": ("uniform", 1 << 20, 4096, 1,
+               "C3: 1M synthetic 8-node systems/GPU, uniform RD/WR over 0x00-0x7F, 4096 instr/core"),
+    "hot": ("hot", 1 << 20, 4096, 1,
+            "C4: 1M hot-line 8-node systems/GPU, RD/WR over {0x00,0x11,0x22,0x33}, 4096 instr/core"),
+    "evict": ("evict", 2 << 20, 4096, 1,
+              "C5: 2M eviction-heavy 8-node systems/GPU (16M on 8), {a: a%4==0}, 4096 instr/core"),
+}
+NP = 8
+
+
+def shard(rank, n_per_rank):
+    """System ids simulated by `rank` (weak scaling: a fixed n_per_rank per GPU)."""
+    return rank * n_per_rank, n_per_rank
+
+
+def reduce_counters(vec, dist_mod=None):
+    """All-reduce a 32-entry uint64 counter vector across ranks: sums (mod 2^64) for every
+    slot except max_rounds (slot 24), which is a max.  `vec` is a torch int64 tensor."""
+    if dist_mod is None or not dist_mod.is_initialized() or dist_mod.get_world_size() == 1:
+        return vec
+    mx = vec[24:25].clone()
+    dist_mod.all_reduce(vec, op=dist_mod.ReduceOp.SUM)
+    dist_mod.all_reduce(mx, op=dist_mod.ReduceOp.MAX)
+    vec[24:25] = mx
+    return vec
+
+
+def cpu_baseline(dist, n_instr, seed, n_sample, threads):
+    """The CPU oracle (clean-room C restatement, gcc -O2 -fopenmp, OpenMP over systems) on a
+    bounded sample of the same system ids -- a reported baseline, not the target."""
+    if ORACLE not in sys.path:
+        sys.path.insert(0, ORACLE)
+    import pyoracle
+    pyoracle.lib()
+    t0 = time.perf_counter()
+    res, _ = pyoracle.run_generated(NP, dist, seed, n_instr, 0, n_sample, nthreads=threads)
+    dt = time.perf_counter() - t0
+    msgs = int(res["msgs"].sum())
+    return res, dict(value=msgs / dt, unit=UNIT, cores=threads, kind="port",
+                     sample=f"systems 0..{n_sample - 1} of the same workload ({msgs} transactions,"
+                            f" {dt:.2f} s wall, {threads} OpenMP threads, traces generated lazily)")
+
+
+def traffic_from_profiles(config):
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get(config)
+        return e if e else None
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="random", choices=sorted(CONFIGS))
+    ap.add_argument("--systems", type=int, default=0, help="override systems per GPU")
+    ap.add_argument("--ring", type=int, default=0)
+    ap.add_argument("--fused", action="store_true",
+                    help="generate instructions inside the transition kernel (no HBM traces)")
+    ap.add_argument("--cpu-sample", type=int, default=262144)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import pydsm
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    dname, n_sys, n_instr, seed, workload = CONFIGS[args.config]
+    if args.systems:
+        n_sys = args.systems
+    first, n_sys = shard(rank, n_sys)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    eng = pydsm.Engine(NP, n_instr, ring_cap=args.ring, device=local, timing=True)
+    cnt = torch.zeros(32, dtype=torch.int64, device=dev)
+    out = torch.empty((n_sys, 4), dtype=torch.int64, device=dev)
+
+    trace_stream = None
+    if not args.fused:
+        traces = torch.empty((n_sys, NP, n_instr), dtype=torch.int16, device=dev)
+        counts = torch.empty((n_sys, NP), dtype=torch.int32, device=dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        eng.generate_device(dname, seed, n_instr, first, n_sys, traces.data_ptr(),
+                            counts.data_ptr(), sp)              # cold (first-touch) pass
+        ev0.record(stream)
+        eng.generate_device(dname, seed, n_instr, first, n_sys, traces.data_ptr(),
+                            counts.data_ptr(), sp)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        gms = ev0.elapsed_time(ev1)
+        gbytes = traces.numel() * 2 + counts.numel() * 4
+        trace_stream = dict(kernel="gen_kernel (trace generator, writes packed traces)",
+                            bytes=gbytes, ms=round(gms, 3),
+                            achieved_gbs=round(gbytes / gms / 1e6, 1), peak_gbs=HBM_PEAK_GBS,
+                            frac=round(gbytes / gms / 1e6 / HBM_PEAK_GBS, 4))
+
+    def step():
+        cnt.zero_()
+        if args.fused:
+            eng.run_generated_device(dname, seed, n_instr, first, n_sys, out.data_ptr(),
+                                     cnt.data_ptr(), sp)
+        else:
+            eng.run_packed_device(traces.data_ptr(), counts.data_ptr(), n_sys, out.data_ptr(),
+                                  cnt.data_ptr(), sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    kms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kms.append(eng.last_kernel_ms())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed_max = float(el.item())
+    local_c = pydsm.counters_to_dict(cnt.cpu().numpy().view(np.uint64))
+    tot = reduce_counters(cnt.clone(), dist if world > 1 else None)
+    c = pydsm.counters_to_dict(tot.cpu().numpy().view(np.uint64))
+
+    if rank == 0:
+        K = args.steps
+        value = c["msgs"] * K / elapsed_max
+        kavg = float(np.mean(kms))
+        alg_bytes = 2 * local_c["instrs"] + (32 + 4 * NP) * local_c["systems"]
+        if args.fused:
+            alg_bytes = 32 * local_c["systems"]
+        ach = alg_bytes / (kavg * 1e-3) / 1e9
+        roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
+                    kernel="sim_kernel<8,16,4,false> (lock-step transition kernel)",
+                    algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),
+                    per_unit="2 B per consumed packed instruction + 32 B result + 4*np B counts per system")
+        tr = traffic_from_profiles(args.config)
+        if tr and not args.fused:
+            roof["traffic"] = tr.get("bytes_per_launch")
+            roof["traffic_source"] = tr.get("source")
+        parity = None
+        if args.config == "random" and rank == 0 and first == 0 and n_sys >= 4096:
+            g = np.load(os.path.join(REPO, "tests", "golden", "ensemble", "np8_uniform.npy"))
+            r = out[:4096].cpu().numpy().view(pydsm.RESULT_DTYPE).reshape(-1)
+            mine = np.stack([r["status"].astype(np.uint64), r["rounds"].astype(np.uint64),
+                             r["msgs"].astype(np.uint64), r["instrs"].astype(np.uint64),
+                             r["dump_hash"], r["final_hash"]], axis=1)
+            parity = "golden[0:4096] bit-exact" if np.array_equal(mine, g) else "GOLDEN MISMATCH"
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            threads = min(16, os.cpu_count() or 1)
+            _, cpu = cpu_baseline(dname, n_instr, seed, min(args.cpu_sample, n_sys), threads)
+        rec = {
+            "metric": METRIC, "value": round(value, 1), "unit": UNIT, "n_gpus": world,
+            "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed_max / K * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (counter-based generator, seed %d)" % seed,
+            "config": {"workload": workload, "systems_per_gpu": n_sys, "np": NP,
+                       "instr_per_node": n_instr, "dist": dname,
+                       "parallelism": f"ensemble-dp{world}",
+                       "traces": "fused generator (no HBM traces)" if args.fused else
+                                 "packed u16 traces resident in HBM"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "trace_stream": trace_stream,
+            "systems_per_s": round(c["systems"] * K / elapsed_max, 1),
+            "instructions_per_s": round(c["instrs"] * K / elapsed_max, 1),
+            "counters": {k: c[k] for k in ("msgs", "instrs", "rounds", "systems", "max_rounds",
+                                           "overflow_reruns", "status_COMPLETED",
+                                           "status_DEADLOCKED")},
+            "sum_final_hash": hex(c["sum_final_hash"]),
+            "parity": parity,
+            "launch": eng.launch_info(),
+        }
+        print(json.dumps(rec), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,109 @@
+/*
+ * cache_simulator.c -- drop-in replacement for the reference's process contract
+ * (ruubhagat/HP-Assignment-2, README.md:86-106, assignment.c:118-123):
+ *
+ *     ./cache_simulator <test_directory>
+ *
+ * reads tests/<test_directory>/core_<n>.txt relative to the CWD (:794), prints
+ * "Processor <n> initialized" per node (:821), simulates the system on the GPU through
+ * libdsm.so under the deterministic lock-step schedule, and writes the printProcessorState
+ * dump core_<n>_output.txt (:824-876) of every node that finished issuing, into the CWD.
+ *
+ * Unlike the reference (whose loop never exits, :153, :584-587) it exits once the system is
+ * quiescent: 0 = every node dumped, 2 = deadlocked (the stuck nodes write no dump, as in the
+ * reference), 3 = ring overflow / assert / round limit, 1 = usage or I/O error.
+ *
+ * Options (all optional; defaults reproduce the reference build):
+ *   --np N           number of nodes, 4 (NUM_PROCS, :9) or 8
+ *   --max-instr N    instructions read per core file, default 32 (MAX_INSTR_NUM, :13)
+ *   --device D       GPU ordinal, default 0
+ *   --quiet          do not print the "initialized" lines
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dsm.h"
+
+static void usage(const char *argv0) {
+    fprintf(stderr, "Usage: %s [--np 4|8] [--max-instr N] [--device D] <test_directory>\n", argv0);
+}
+
+int main(int argc, char **argv) {
+    int np = 4, device = 0, quiet = 0;
+    uint32_t max_instr = DSM_REF_MAX_INSTR;
+    const char *dir = NULL;
+    for (int i = 1; i < argc; ++i) {
+        if (!strcmp(argv[i], "--np") && i + 1 < argc) np = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--max-instr") && i + 1 < argc) max_instr = (uint32_t)atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--device") && i + 1 < argc) device = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--quiet")) quiet = 1;
+        else if (argv[i][0] == '-' && argv[i][1] == '-') { usage(argv[0]); return EXIT_FAILURE; }
+        else dir = argv[i];
+    }
+    if (!dir) { usage(argv[0]); return EXIT_FAILURE; }                 /* :119-122 */
+    if ((np != 4 && np != 8) || max_instr == 0 || max_instr > DSM_MAX_INSTR) {
+        usage(argv[0]);
+        return EXIT_FAILURE;
+    }
+    const uint32_t stride = (max_instr + 7u) & ~7u;
+    uint16_t *traces = (uint16_t *)calloc((size_t)np * stride, sizeof(uint16_t));
+    uint32_t counts[DSM_MAX_NP] = {0};
+    if (!traces) return EXIT_FAILURE;
+
+    for (int n = 0; n < np; ++n) {
+        char path[256];
+        snprintf(path, sizeof path, "tests/%s/core_%d.txt", dir, n);   /* :794 */
+        int rc = dsm_parse_trace_file(path, traces + (size_t)n * stride, max_instr, &counts[n]);
+        if (rc == DSM_E_IO) {                                          /* :796-800 */
+            fprintf(stderr, "Error: could not open file %s\n", path);
+            perror("fopen");
+            exit(EXIT_FAILURE);
+        }
+        if (rc) {
+            fprintf(stderr, "Error: %s: %s\n", path, dsm_strerror(rc));
+            exit(EXIT_FAILURE);
+        }
+        for (uint32_t i = 0; i < counts[n]; ++i)
+            if (((traces[(size_t)n * stride + i] >> 12) & 7u) >= (unsigned)np) {
+                fprintf(stderr, "Error: %s: %s\n", path, dsm_strerror(DSM_E_RANGE));
+                exit(EXIT_FAILURE);
+            }
+        if (!quiet) printf("Processor %d initialized\n", n);           /* :821 */
+    }
+    fflush(stdout);
+
+    dsm_config cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.np = np;
+    cfg.max_instr = stride;
+    cfg.flags = DSM_F_SNAPSHOTS;
+    dsm_ctx *ctx = NULL;
+    int rc = dsm_open(device, &cfg, &ctx);
+    if (rc) {
+        fprintf(stderr, "Error: dsm_open: %s\n", dsm_strerror(rc));
+        return EXIT_FAILURE;
+    }
+    dsm_sys_result res;
+    rc = dsm_run_packed(ctx, traces, counts, 1, &res, NULL);
+    if (rc) {
+        fprintf(stderr, "Error: dsm_run_packed: %s\n", dsm_strerror(rc));
+        dsm_close(ctx);
+        return EXIT_FAILURE;
+    }
+    const uint32_t status = res.status & 0xFFu, dumped = res.status >> 8;
+    for (int n = 0; n < np; ++n) {
+        if (!((dumped >> n) & 1u)) continue;
+        dsm_node_state st;
+        if ((rc = dsm_get_node_state(ctx, 0, n, &st, NULL)) || (rc = dsm_write_dump(n, &st, NULL))) {
+            fprintf(stderr, "Error: dump of node %d: %s\n", n, dsm_strerror(rc));
+            dsm_close(ctx);
+            return EXIT_FAILURE;
+        }
+    }
+    dsm_close(ctx);
+    free(traces);
+    if (status == DSM_COMPLETED) return 0;
+    if (status == DSM_DEADLOCKED) return 2;
+    return 3;
+}

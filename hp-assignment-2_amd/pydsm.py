@@ -1,0 +1,237 @@
+"""pydsm -- thin ctypes binding of libdsm.so (include/dsm.h) for tests, bench.py and smoke().
+
+This is plumbing, not the product: the engine is the C ABI over the gfx950 HIP kernels.
+There is deliberately no fallback of any kind: if libdsm.so is missing, or the device is not
+a gfx950, every engine call raises DsmError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdsm.so")
+CLI_PATH = os.path.join(HERE, "cache_simulator")
+
+NTYPES = 13
+TYPE_NAMES = ["READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID", "INV",
+              "UPGRADE", "WRITEBACK_INV", "WRITEBACK_INT", "FLUSH", "FLUSH_INVACK",
+              "EVICT_SHARED", "EVICT_MODIFIED"]
+STATUS_NAMES = ["COMPLETED", "DEADLOCKED", "RING_OVERFLOW", "ASSERT_FAILED", "ROUND_LIMIT"]
+DIST = {"uniform": 0, "hot": 1, "evict": 2}
+F_SNAPSHOTS = 1
+F_TIMING = 2
+
+RESULT_DTYPE = np.dtype([("status", "<u4"), ("rounds", "<u4"), ("msgs", "<u4"),
+                         ("instrs", "<u4"), ("dump_hash", "<u8"), ("final_hash", "<u8")])
+COUNTER_FIELDS = ([f"msgs_{t}" for t in TYPE_NAMES] +
+                  ["msgs", "instrs", "rounds", "systems"] +
+                  [f"status_{s}" for s in STATUS_NAMES] +
+                  ["sum_dump_hash", "sum_final_hash", "max_rounds", "overflow_reruns"] +
+                  [f"reserved{i}" for i in range(6)])
+assert len(COUNTER_FIELDS) == 32
+
+E_INVAL, E_DEVICE, E_NOMEM, E_IO, E_FORMAT, E_STATE, E_RANGE = -1, -2, -3, -4, -5, -6, -7
+
+
+class DsmError(RuntimeError):
+    def __init__(self, code, what):
+        self.code = code
+        super().__init__(f"{what}: {strerror(code)} ({code})")
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("np", ctypes.c_int), ("max_instr", ctypes.c_uint32),
+                ("ring_cap", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class Gen(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("dist", ctypes.c_int), ("n_instr", ctypes.c_uint32)]
+
+
+class LaunchInfo(ctypes.Structure):
+    _fields_ = [("grid_blocks", ctypes.c_int), ("block_threads", ctypes.c_int),
+                ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int),
+                ("ring_cap", ctypes.c_int), ("lds_bytes_per_block", ctypes.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libdsm.so (raises if it has not been built: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not built (run `make -C hp-assignment-2_amd`)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        sig = {
+            "dsm_abi_version": (i32, []),
+            "dsm_strerror": (ctypes.c_char_p, [i32]),
+            "dsm_device_count": (i32, [ctypes.POINTER(i32)]),
+            "dsm_open": (i32, [i32, ctypes.POINTER(Config), ctypes.POINTER(vp)]),
+            "dsm_close": (None, [vp]),
+            "dsm_launch_info_get": (i32, [vp, ctypes.POINTER(LaunchInfo)]),
+            "dsm_run_packed": (i32, [vp, vp, vp, u64, vp, vp]),
+            "dsm_run_packed_device": (i32, [vp, vp, vp, u64, vp, vp, vp]),
+            "dsm_generate_device": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp, vp]),
+            "dsm_run_generated_device": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp, vp]),
+            "dsm_run_generated": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp]),
+            "dsm_get_node_state": (i32, [vp, u64, i32, vp, vp]),
+            "dsm_last_kernel_ms": (i32, [vp, ctypes.POINTER(ctypes.c_float)]),
+            "dsm_parse_trace_file": (i32, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
+            "dsm_load_test_dir": (i32, [ctypes.c_char_p, i32, u32, vp, u32, vp]),
+            "dsm_format_dump": (i32, [i32, vp, ctypes.c_char_p, ctypes.c_size_t]),
+            "dsm_write_dump": (i32, [i32, vp, ctypes.c_char_p]),
+            "dsm_node_hash": (u64, [i32, vp, i32]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def strerror(code):
+    try:
+        return lib().dsm_strerror(code).decode()
+    except OSError:
+        return "libdsm.so unavailable"
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise DsmError(rc, what)
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def counters_to_dict(c):
+    c = np.asarray(c, dtype=np.uint64).reshape(-1)
+    return {k: int(v) for k, v in zip(COUNTER_FIELDS, c) if not k.startswith("reserved")}
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(lib().dsm_device_count(ctypes.byref(n)), "dsm_device_count")
+    return n.value
+
+
+class Engine:
+    """One dsm_ctx: np nodes per system, trace stride max_instr, bound to `device`."""
+
+    def __init__(self, np_=8, max_instr=4096, ring_cap=0, snapshots=False, device=0, timing=False):
+        self.np = np_
+        self.max_instr = max_instr
+        self.cfg = Config(np_, max_instr, ring_cap,
+                          (F_SNAPSHOTS if snapshots else 0) | (F_TIMING if timing else 0))
+        self.ctx = ctypes.c_void_p()
+        _check(lib().dsm_open(device, ctypes.byref(self.cfg), ctypes.byref(self.ctx)), "dsm_open")
+
+    def close(self):
+        if self.ctx:
+            lib().dsm_close(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host-buffer entry points ----------------------------------------------------------
+    def run_packed(self, traces, counts):
+        traces = np.ascontiguousarray(traces, dtype=np.uint16)
+        counts = np.ascontiguousarray(counts, dtype=np.uint32)
+        n = counts.shape[0]
+        assert traces.shape == (n, self.np, self.max_instr), traces.shape
+        assert counts.shape == (n, self.np)
+        res = np.zeros(n, dtype=RESULT_DTYPE)
+        cnt = np.zeros(32, dtype=np.uint64)
+        _check(lib().dsm_run_packed(self.ctx, _ptr(traces), _ptr(counts), n, _ptr(res), _ptr(cnt)),
+               "dsm_run_packed")
+        return res, counters_to_dict(cnt)
+
+    def run_generated(self, dist, seed, n_instr, first_sys, n_sys):
+        g = Gen(seed, DIST.get(dist, dist), n_instr)
+        res = np.zeros(n_sys, dtype=RESULT_DTYPE)
+        cnt = np.zeros(32, dtype=np.uint64)
+        _check(lib().dsm_run_generated(self.ctx, ctypes.byref(g), first_sys, n_sys, _ptr(res),
+                                       _ptr(cnt)), "dsm_run_generated")
+        return res, counters_to_dict(cnt)
+
+    # -- device-pointer entry points (torch-owned HBM, torch streams) ----------------------
+    def generate_device(self, dist, seed, n_instr, first_sys, n_sys, d_traces, d_counts, stream=0):
+        g = Gen(seed, DIST.get(dist, dist), n_instr)
+        _check(lib().dsm_generate_device(self.ctx, ctypes.byref(g), first_sys, n_sys,
+                                         ctypes.c_void_p(d_traces), ctypes.c_void_p(d_counts),
+                                         ctypes.c_void_p(stream)), "dsm_generate_device")
+
+    def run_packed_device(self, d_traces, d_counts, n_sys, d_results, d_counters, stream=0):
+        _check(lib().dsm_run_packed_device(self.ctx, ctypes.c_void_p(d_traces),
+                                           ctypes.c_void_p(d_counts), n_sys,
+                                           ctypes.c_void_p(d_results), ctypes.c_void_p(d_counters),
+                                           ctypes.c_void_p(stream)), "dsm_run_packed_device")
+
+    def run_generated_device(self, dist, seed, n_instr, first_sys, n_sys, d_results, d_counters,
+                             stream=0):
+        g = Gen(seed, DIST.get(dist, dist), n_instr)
+        _check(lib().dsm_run_generated_device(self.ctx, ctypes.byref(g), first_sys, n_sys,
+                                              ctypes.c_void_p(d_results),
+                                              ctypes.c_void_p(d_counters),
+                                              ctypes.c_void_p(stream)), "dsm_run_generated_device")
+
+    def node_state(self, sys, node):
+        d = np.zeros(64, dtype=np.uint8)
+        f = np.zeros(64, dtype=np.uint8)
+        _check(lib().dsm_get_node_state(self.ctx, sys, node, _ptr(d), _ptr(f)), "dsm_get_node_state")
+        return d, f
+
+    def last_kernel_ms(self):
+        ms = ctypes.c_float(0)
+        _check(lib().dsm_last_kernel_ms(self.ctx, ctypes.byref(ms)), "dsm_last_kernel_ms")
+        return float(ms.value)
+
+    def launch_info(self):
+        li = LaunchInfo()
+        _check(lib().dsm_launch_info_get(self.ctx, ctypes.byref(li)), "dsm_launch_info_get")
+        return {k: getattr(li, k) for k, _ in LaunchInfo._fields_}
+
+
+# -- host-only boundary helpers ------------------------------------------------------------
+def parse_trace_file(path, cap=32):
+    out = np.zeros(max(cap, 1), dtype=np.uint16)
+    n = ctypes.c_uint32(0)
+    rc = lib().dsm_parse_trace_file(path.encode(), _ptr(out), cap, ctypes.byref(n))
+    _check(rc, f"dsm_parse_trace_file({path})")
+    return out[:n.value].copy()
+
+
+def format_dump(node, rec):
+    rec = np.ascontiguousarray(rec, dtype=np.uint8)
+    assert rec.size == 64
+    buf = ctypes.create_string_buffer(4096)
+    n = lib().dsm_format_dump(node, _ptr(rec), buf, 4096)
+    if n < 0:
+        raise DsmError(n, "dsm_format_dump")
+    return buf.raw[:n].decode()
+
+
+def node_hash(node, rec, nwords):
+    rec = np.ascontiguousarray(rec, dtype=np.uint8)
+    return int(lib().dsm_node_hash(node, _ptr(rec), nwords))
+
+
+def pack_instr(op, addr, value=0):
+    """'R'/'W' + address + value -> packed u16 (bit15 WR, bits 8-14 address, bits 0-7 value)."""
+    wr = 1 if op in ("W", "WR") else 0
+    return (wr << 15) | ((addr & 0x7F) << 8) | ((value & 0xFF) if wr else 0)

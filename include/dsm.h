@@ -1,0 +1,214 @@
+/*
+ * include/dsm.h -- C ABI of the MI355X-native ensemble coherence simulator (libdsm.so).
+ *
+ * The reference (ruubhagat/HP-Assignment-2, assignment.c) has no plugin or FFI API: its
+ * whole boundary is the process contract `./cache_simulator <test_directory>` plus four
+ * internal C functions.  Each entry point below names the reference interface it replaces:
+ *
+ *   dsm_parse_trace_file / dsm_load_test_dir  <- initializeProcessor   assignment.c:776-822
+ *   dsm_format_dump / dsm_write_dump          <- printProcessorState   assignment.c:824-876
+ *   dsm_run_* (lock-step ensemble engine)     <- the per-node loop of main (:135-699), the
+ *                                                message switch (:177-566), instruction issue
+ *                                                (:590-687), handleCacheReplacement
+ *                                                (:742-773) and sendMessage (:711-739)
+ *   dsm_get_node_state                        <- the processorNode snapshot handed to
+ *                                                printProcessorState by value (:695)
+ *
+ * Conventions: plain C types only; every function returns 0 (DSM_OK) or a negative DSM_E_*
+ * code (dsm_strerror); nothing throws across the ABI.  A dsm_ctx owns its device memory, is
+ * bound to one GPU and must be used from one host thread at a time (not reentrant).  The
+ * engine runs on hand-written gfx950 HIP kernels only: there is no CPU fallback, and when the
+ * device cannot be used the run functions fail with DSM_E_DEVICE.
+ */
+#ifndef DSM_H
+#define DSM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSM_ABI_VERSION 1
+
+#define DSM_MAX_NP 8             /* bitVector is one byte (README.md:51)                  */
+#define DSM_CACHE_SIZE 4         /* CACHE_SIZE      assignment.c:10                        */
+#define DSM_MEM_SIZE 16          /* MEM_SIZE        assignment.c:11                        */
+#define DSM_REF_RING_CAP 256     /* MSG_BUFFER_SIZE assignment.c:12                        */
+#define DSM_REF_MAX_INSTR 32     /* MAX_INSTR_NUM   assignment.c:13                        */
+#define DSM_MAX_INSTR 4096       /* longest per-node trace the engine accepts               */
+#define DSM_NTYPES 13            /* transactionType assignment.c:20-34                     */
+#define DSM_MAX_ROUNDS (1u << 22)  /* active rounds before DSM_ROUND_LIMIT is reported */
+
+/* return codes */
+enum {
+    DSM_OK = 0,
+    DSM_E_INVAL = -1,    /* bad argument or configuration                                  */
+    DSM_E_DEVICE = -2,   /* no usable gfx950 device / HIP runtime error                     */
+    DSM_E_NOMEM = -3,    /* device or host allocation failed                                */
+    DSM_E_IO = -4,       /* trace or dump file could not be opened / written                */
+    DSM_E_FORMAT = -5,   /* trace line the reference would not parse into an instruction    */
+    DSM_E_STATE = -6,    /* e.g. dsm_get_node_state without DSM_F_SNAPSHOTS                  */
+    DSM_E_RANGE = -7     /* address whose home node is >= np (assignment.c:90 would overrun) */
+};
+
+/* per-system status (dsm_sys_result.status bits 0..7); bits 8..15 = mask of dumped nodes */
+enum {
+    DSM_COMPLETED = 0,      /* every node issued all instructions and dumped (:688-697)     */
+    DSM_DEADLOCKED = 1,     /* quiescent with some node still waitingForReply (:578-581)    */
+    DSM_RING_OVERFLOW = 2,  /* an inbox would exceed MSG_BUFFER_SIZE (:715-724)              */
+    DSM_ASSERT_FAILED = 3,  /* a reference assert() would have aborted (:189,:443,:489,...) */
+    DSM_ROUND_LIMIT = 4     /* DSM_MAX_ROUNDS active rounds without quiescence             */
+};
+
+/* transactionType, assignment.c:20-34 (same numeric values) */
+enum {
+    DSM_READ_REQUEST = 0, DSM_WRITE_REQUEST, DSM_REPLY_RD, DSM_REPLY_WR, DSM_REPLY_ID, DSM_INV,
+    DSM_UPGRADE, DSM_WRITEBACK_INV, DSM_WRITEBACK_INT, DSM_FLUSH, DSM_FLUSH_INVACK,
+    DSM_EVICT_SHARED, DSM_EVICT_MODIFIED
+};
+
+/* synthetic address distributions (BASELINE.json configs) */
+enum { DSM_DIST_UNIFORM = 0, DSM_DIST_HOT = 1, DSM_DIST_EVICT = 2 };
+
+/* config flags */
+#define DSM_F_SNAPSHOTS 1u  /* keep per-node dump + final records of the last run          */
+#define DSM_F_TIMING 2u     /* record HIP events around the transition kernel of each run     */
+
+typedef struct dsm_config {
+    int np;              /* NUM_PROCS: 4 or 8                                               */
+    uint32_t max_instr;  /* per-node trace slot (stride) in instructions; multiple of 8,
+                            <= DSM_MAX_INSTR                                                */
+    uint32_t ring_cap;   /* inbox depth of the fast kernel: 0 (= 16), 8, 16 or 32.  Systems
+                            that would overflow it are re-run on the device with the
+                            reference depth 256; only overflow beyond 256 is reported.     */
+    uint32_t flags;      /* DSM_F_*                                                         */
+} dsm_config;
+
+/* counter-based trace generator: instruction i of node n of system s depends only on
+ * (seed, dist, np, s, n, i), so results do not depend on batching or GPU count. */
+typedef struct dsm_gen {
+    uint64_t seed;
+    int dist;            /* DSM_DIST_*                                                      */
+    uint32_t n_instr;    /* instructions per node, <= DSM_MAX_INSTR                         */
+} dsm_gen;
+
+/* per-system result, 32 bytes */
+typedef struct dsm_sys_result {
+    uint32_t status;     /* DSM_COMPLETED.. | dumped-node mask << 8                         */
+    uint32_t rounds;     /* active lock-step rounds                                         */
+    uint32_t msgs;       /* messages handled (transactions)                                 */
+    uint32_t instrs;     /* instructions issued                                             */
+    uint64_t dump_hash;  /* sum over dumped nodes of dsm_node_hash(node, dump, 15)          */
+    uint64_t final_hash; /* sum over nodes of dsm_node_hash(node, final, 16)                */
+} dsm_sys_result;
+
+/* canonical node record, 64 bytes; field meanings from processorNode (assignment.c:70-81) */
+typedef struct dsm_node_state {
+    uint8_t memory[DSM_MEM_SIZE];      /* node.memory                                       */
+    uint8_t dir_bv[DSM_MEM_SIZE];      /* directory[i].bitVector                            */
+    uint8_t dir_state[DSM_MEM_SIZE];   /* directory[i].state: EM=0, S=1, U=2 (:18)          */
+    uint8_t cache_addr[DSM_CACHE_SIZE];
+    uint8_t cache_value[DSM_CACHE_SIZE];
+    uint8_t cache_state[DSM_CACHE_SIZE]; /* MODIFIED=0, EXCLUSIVE=1, SHARED=2, INVALID=3    */
+    uint8_t pending;                   /* pendingWriteValue                                 */
+    uint8_t flags;                     /* bit0 waitingForReply, bit1 dumped                 */
+    uint16_t issued;                   /* instructions issued (instructionIdx + 1)          */
+} dsm_node_state;
+
+/* aggregate counters (all sums except max_rounds); 32 x uint64 */
+typedef struct dsm_counters {
+    uint64_t msgs_by_type[DSM_NTYPES];
+    uint64_t msgs;
+    uint64_t instrs;
+    uint64_t rounds;
+    uint64_t systems;
+    uint64_t by_status[5];
+    uint64_t sum_dump_hash;    /* mod 2^64 */
+    uint64_t sum_final_hash;   /* mod 2^64 */
+    uint64_t max_rounds;       /* max, not sum */
+    uint64_t overflow_reruns;  /* systems re-run with the 256-deep inbox */
+    uint64_t reserved[6];
+} dsm_counters;
+
+typedef struct dsm_ctx dsm_ctx;
+
+/* launch geometry of the last run (for measurement / roofline accounting) */
+typedef struct dsm_launch_info {
+    int grid_blocks;       /* persistent workgroups of the transition kernel               */
+    int block_threads;
+    int waves_per_cu;      /* resident waves per CU the occupancy query allowed            */
+    int cus;
+    int ring_cap;
+    int lds_bytes_per_block;
+} dsm_launch_info;
+
+/* ---- library ---------------------------------------------------------------------- */
+int dsm_abi_version(void);
+const char *dsm_strerror(int code);
+int dsm_device_count(int *count);
+
+/* ---- engine context (GPU) ---------------------------------------------------------- */
+int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out);
+void dsm_close(dsm_ctx *ctx);
+int dsm_launch_info_get(dsm_ctx *ctx, dsm_launch_info *info);
+
+/* Host buffers: traces [n_sys][np][max_instr] packed u16 (bit15 WR, bits8-14 address,
+ * bits0-7 value), counts [n_sys][np].  Copies in, runs, copies out, synchronises.
+ * per_sys (n_sys entries) and out may be NULL; out is overwritten. */
+int dsm_run_packed(dsm_ctx *ctx, const uint16_t *traces, const uint32_t *counts,
+                   uint64_t n_sys, dsm_sys_result *per_sys, dsm_counters *out);
+
+/* Device buffers (e.g. torch-owned HBM), asynchronous on `stream` (hipStream_t; NULL =
+ * null stream).  d_results may be NULL; d_counters (device, one dsm_counters) is
+ * ACCUMULATED into.  No host synchronisation inside. */
+int dsm_run_packed_device(dsm_ctx *ctx, const uint16_t *d_traces, const uint32_t *d_counts,
+                          uint64_t n_sys, dsm_sys_result *d_results,
+                          dsm_counters *d_counters, void *stream);
+
+/* GPU trace generator: writes d_traces [n_sys][np][max_instr] and d_counts [n_sys][np]
+ * for systems first_sys .. first_sys+n_sys-1 (requires gen->n_instr <= max_instr). */
+int dsm_generate_device(dsm_ctx *ctx, const dsm_gen *gen, uint64_t first_sys, uint64_t n_sys,
+                        uint16_t *d_traces, uint32_t *d_counts, void *stream);
+
+/* Engine with the generator fused in (instructions computed when issued; no trace bytes). */
+int dsm_run_generated_device(dsm_ctx *ctx, const dsm_gen *gen, uint64_t first_sys,
+                             uint64_t n_sys, dsm_sys_result *d_results,
+                             dsm_counters *d_counters, void *stream);
+int dsm_run_generated(dsm_ctx *ctx, const dsm_gen *gen, uint64_t first_sys, uint64_t n_sys,
+                      dsm_sys_result *per_sys, dsm_counters *out);
+
+/* Snapshot of node `node` of system `sys` of the last run (needs DSM_F_SNAPSHOTS):
+ * `dump` = state when the node finished issuing (what printProcessorState prints, :695),
+ * `final_state` = state when the system stopped.  Either pointer may be NULL. */
+int dsm_get_node_state(dsm_ctx *ctx, uint64_t sys, int node, dsm_node_state *dump,
+                       dsm_node_state *final_state);
+
+/* Device time of the transition kernel of the last run (needs DSM_F_TIMING): HIP events
+ * recorded on the run's own stream right before and after the kernel launch.  Waits for
+ * the stop event. */
+int dsm_last_kernel_ms(dsm_ctx *ctx, float *ms);
+
+/* ---- boundary helpers (host only; no GPU needed) ----------------------------------- */
+/* initializeProcessor's parser (:802-818): 20-byte fgets chunks, "RD %hhx" / "WR %hhx %hhu"
+ * (mod-256 wrap), at most `cap` instructions (extra lines silently dropped as :805 does).
+ * A chunk that is neither RD nor WR is DSM_E_FORMAT (the reference would count an
+ * uninitialised instruction).  Missing file: DSM_E_IO. */
+int dsm_parse_trace_file(const char *path, uint16_t *out, uint32_t cap, uint32_t *count);
+/* tests/<dir_name>/core_<n>.txt for n < np, relative to the CWD (:794); addresses must
+ * have home < np (DSM_E_RANGE).  traces [np][stride], counts [np]. */
+int dsm_load_test_dir(const char *dir_name, int np, uint32_t cap, uint16_t *traces,
+                      uint32_t stride, uint32_t *counts);
+/* byte-exact printProcessorState text (:839-873); returns length, or DSM_E_INVAL if cap is
+ * too small */
+int dsm_format_dump(int node, const dsm_node_state *st, char *buf, size_t cap);
+/* writes core_<node>_output.txt (:831) into directory `dir` (NULL = CWD) */
+int dsm_write_dump(int node, const dsm_node_state *st, const char *dir);
+/* 64-bit hash of the first nwords (15: dump view, 16: final view) u32 words of a record */
+uint64_t dsm_node_hash(int node, const dsm_node_state *st, int nwords);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -40,7 +40,8 @@
 #define MSG_BUFFER_SIZE 256
 
 /* asserts of the regular build abort the process; here they end the system with
- * ST_ASSERT_FAILED (the enclosing handler returns at the failed assert). */
+ * ST_ASSERT_FAILED at the end of the round (the enclosing handler returns at the failed
+ * assert; the other nodes finish their actions of that round; nothing is delivered). */
 static int g_assert_failed;
 #define assert(e) do { if (!(e)) { g_assert_failed = 1; return; } } while (0)
 
@@ -158,7 +159,6 @@ static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
                 if (c->instructionIdx != before) instrs++;
                 acted = 1;
             }
-            if (g_assert_failed) break;
         }
         if (g_assert_failed) { status = ST_ASSERT_FAILED; rounds = r; break; }
         int ovf = (nst > MAX_STAGED);

@@ -1,0 +1,160 @@
+"""Host side of the drop-in boundary (no GPU): libdsm.so loads and exports every symbol of
+include/dsm.h; the trace parser follows initializeProcessor (assignment.c:802-818); the dump
+formatter is byte-identical to printProcessorState (:824-876); the hash matches the oracle's.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import pydsm
+import pyoracle as orc
+from conftest import PKG, REPO, TESTS, golden_dump, golden_records, inputs_dir
+
+
+def header_functions():
+    txt = open(os.path.join(REPO, "include", "dsm.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(dsm_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for f in ["dsm_open", "dsm_close", "dsm_run_packed", "dsm_run_packed_device",
+              "dsm_generate_device", "dsm_run_generated", "dsm_run_generated_device",
+              "dsm_get_node_state", "dsm_parse_trace_file", "dsm_load_test_dir",
+              "dsm_format_dump", "dsm_write_dump", "dsm_node_hash", "dsm_strerror"]:
+        assert f in fns
+
+
+def test_library_exports_every_header_symbol():
+    L = pydsm.lib()
+    missing = [f for f in header_functions() if not hasattr(L, f)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", pydsm.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert set(header_functions()) <= exported
+
+
+def test_abi_version_and_errors():
+    L = pydsm.lib()
+    assert L.dsm_abi_version() == 1
+    assert pydsm.strerror(0) == "ok"
+    for code in range(-7, 0):
+        assert pydsm.strerror(code) != "unknown error"
+
+
+@pytest.mark.parametrize("test", TESTS)
+def test_parser_reads_reference_inputs(test):
+    for core in range(4):
+        p = os.path.join(inputs_dir(test), f"core_{core}.txt")
+        mine = pydsm.parse_trace_file(p, 32)
+        ref = orc.parse_core_file(p, 32)
+        assert list(mine) == ref
+
+
+def _write(tmp_path, name, text):
+    p = tmp_path / name
+    p.write_bytes(text.encode())
+    return str(p)
+
+
+def test_parser_semantics(tmp_path):
+    # %hhu wraps modulo 256 and %hhx takes the 0x prefix (:807, :812)
+    p = _write(tmp_path, "a.txt", "WR 0x15 300\nRD 0x17\nWR 0x01 255\n")
+    got = pydsm.parse_trace_file(p, 32)
+    assert list(got) == [pydsm.pack_instr("W", 0x15, 300 % 256), pydsm.pack_instr("R", 0x17),
+                         pydsm.pack_instr("W", 0x01, 255)]
+    # more than MAX_INSTR_NUM lines are silently truncated (:805)
+    p = _write(tmp_path, "b.txt", "".join(f"RD 0x{i % 64:02X}\n" for i in range(40)))
+    assert len(pydsm.parse_trace_file(p, 32)) == 32
+    assert len(pydsm.parse_trace_file(p, 64)) == 40
+    # empty file: zero instructions (tests/sample/core_2.txt)
+    assert len(pydsm.parse_trace_file(_write(tmp_path, "c.txt", ""), 32)) == 0
+    # a chunk that is neither RD nor WR: the reference would count garbage -> rejected
+    with pytest.raises(pydsm.DsmError) as e:
+        pydsm.parse_trace_file(_write(tmp_path, "d.txt", "RD 0x01\n\nRD 0x02\n"), 32)
+    assert e.value.code == pydsm.E_FORMAT
+    # missing file (:796-800)
+    with pytest.raises(pydsm.DsmError) as e:
+        pydsm.parse_trace_file(str(tmp_path / "nope.txt"), 32)
+    assert e.value.code == pydsm.E_IO
+    # addresses beyond 8 nodes cannot be simulated (bitVector is one byte)
+    with pytest.raises(pydsm.DsmError) as e:
+        pydsm.parse_trace_file(_write(tmp_path, "e.txt", "RD 0x90\n"), 32)
+    assert e.value.code == pydsm.E_RANGE
+
+
+def test_load_test_dir_range_check(tmp_path):
+    d = tmp_path / "tests" / "t"
+    d.mkdir(parents=True)
+    for n in range(8):
+        (d / f"core_{n}.txt").write_text("RD 0x45\n" if n == 0 else "")
+    tr = np.zeros((8, 32), dtype=np.uint16)
+    cn = np.zeros(8, dtype=np.uint32)
+    cwd = os.getcwd()
+    try:
+        os.chdir(tmp_path)
+        rc = pydsm.lib().dsm_load_test_dir(b"t", 4, 32, ctypes.c_void_p(tr.ctypes.data), 32,
+                                          ctypes.c_void_p(cn.ctypes.data))
+        assert rc == pydsm.E_RANGE      # home node 4 does not exist with NUM_PROCS=4
+        rc = pydsm.lib().dsm_load_test_dir(b"t", 8, 32, ctypes.c_void_p(tr.ctypes.data), 32,
+                                          ctypes.c_void_p(cn.ctypes.data))
+        assert rc == 0 and cn[0] == 1
+    finally:
+        os.chdir(cwd)
+
+
+@pytest.mark.parametrize("test", TESTS)
+def test_formatter_byte_exact(test):
+    recs = golden_records(test)
+    for core in range(4):
+        assert pydsm.format_dump(core, recs[0, core]) == golden_dump(test, core)
+
+
+def test_write_dump(tmp_path):
+    recs = golden_records("test_4")
+    rc = pydsm.lib().dsm_write_dump(3, ctypes.c_void_p(recs[0, 3].ctypes.data), str(tmp_path).encode())
+    assert rc == 0
+    assert (tmp_path / "core_3_output.txt").read_text() == golden_dump("test_4", 3)
+
+
+def test_hash_matches_oracle():
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        rec = rng.integers(0, 256, 64, dtype=np.uint8)
+        node = int(rng.integers(0, 8))
+        for nw in (15, 16):
+            assert pydsm.node_hash(node, rec, nw) == orc.hash_rec(node, rec, nw)
+
+
+def test_no_gpu_means_loud_failure():
+    """Without a usable gfx950 the engine refuses to run (no CPU fallback)."""
+    if pydsm.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(pydsm.DsmError) as e:
+        pydsm.Engine(8, 64)
+    assert e.value.code == pydsm.E_DEVICE
+
+
+def test_cli_without_gpu_fails_loudly(tmp_path):
+    if pydsm.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    os.symlink(os.path.join(REPO, "tests", "golden", "inputs"), tmp_path / "tests")
+    r = subprocess.run([pydsm.CLI_PATH, "sample"], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 1
+    assert "dsm_open" in r.stderr
+    assert r.stdout.splitlines() == [f"Processor {n} initialized" for n in range(4)]
+    assert not list(tmp_path.glob("core_*_output.txt"))
+
+
+def test_cli_usage_and_missing_input(tmp_path):
+    r = subprocess.run([pydsm.CLI_PATH], capture_output=True, text=True)
+    assert r.returncode == 1 and "Usage" in r.stderr
+    r = subprocess.run([pydsm.CLI_PATH, "nosuch"], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 1
+    assert "Error: could not open file tests/nosuch/core_0.txt" in r.stderr
