@@ -122,18 +122,23 @@ DEVI uint64_t splitmix(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
+/* One splitmix64 output feeds 4 consecutive instructions, 16 bits each. */
 template <int NP>
-DEVI uint32_t gen_instr(uint64_t seed, int dist, uint64_t sys, uint32_t node, uint32_t idx) {
-    const uint64_t key = (sys << 16) | ((uint64_t)node << 12) | (uint64_t)(idx & 0xFFF);
-    const uint64_t r = splitmix(seed * 0x9E3779B97F4A7C15ULL + key);
-    const uint32_t wr = (uint32_t)r & 1u;
-    const uint32_t val = wr ? (uint32_t)(r >> 8) & 0xFFu : 0u;
-    const uint32_t sel = (uint32_t)(r >> 32);
+DEVI uint32_t instr_from_bits(uint32_t h, int dist) {
+    const uint32_t wr = h & 1u;
+    const uint32_t val = wr ? (h >> 1) & 0xFFu : 0u;
+    const uint32_t sel = h >> 9;
     uint32_t addr;
     if (dist == DSM_DIST_HOT) addr = (sel & 3u) * 0x11u;
     else if (dist == DSM_DIST_EVICT) addr = (sel & (uint32_t)(NP * 4 - 1)) * 4u;
     else addr = sel & (uint32_t)(NP * 16 - 1);
     return (wr << 15) | (addr << 8) | val;
+}
+template <int NP>
+DEVI uint32_t gen_instr(uint64_t seed, int dist, uint64_t sys, uint32_t node, uint32_t idx) {
+    const uint64_t key = (sys << 16) | ((uint64_t)node << 12) | (uint64_t)((idx & 0xFFFu) >> 2);
+    const uint64_t r = splitmix(seed * 0x9E3779B97F4A7C15ULL + key);
+    return instr_from_bits<NP>((uint32_t)(r >> (16 * (idx & 3u))) & 0xFFFFu, dist);
 }
 
 struct Node {
@@ -150,33 +155,37 @@ struct Node {
     uint64_t dh;      /* hash of the dump snapshot                                          */
 };
 
-/* canonical 64-byte record (dsm_node_state) as 16 words */
-DEVI void build_rec(const Node &nd, uint32_t flags, uint32_t (&w)[16]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { w[k] = nd.mem[k]; w[4 + k] = nd.bv[k]; }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t e = nd.dst >> (8 * k);
-        w[8 + k] = (e & 3u) | (((e >> 2) & 3u) << 8) | (((e >> 4) & 3u) << 16) |
-                   (((e >> 6) & 3u) << 24);
+/* canonical 64-byte record (dsm_node_state) word i (i is a compile-time constant after
+ * unrolling, so the switch folds away and no 16-register record is ever live) */
+DEVI uint32_t rec_word(const Node &nd, uint32_t flags, int i) {
+    switch (i) {
+    case 0: case 1: case 2: case 3: return nd.mem[i];
+    case 4: case 5: case 6: case 7: return nd.bv[i - 4];
+    case 8: case 9: case 10: case 11: {
+        const uint32_t e = nd.dst >> (8 * (i - 8));
+        return (e & 3u) | (((e >> 2) & 3u) << 8) | (((e >> 4) & 3u) << 16) | (((e >> 6) & 3u) << 24);
     }
-    w[12] = nd.caddr;
-    w[13] = nd.cval;
-    w[14] = (nd.cst & 3u) | (((nd.cst >> 2) & 3u) << 8) | (((nd.cst >> 4) & 3u) << 16) |
-            (((nd.cst >> 6) & 3u) << 24);
-    w[15] = (nd.ctl & 0xFFu) | (flags << 8) | (nd.ip << 16);
+    case 12: return nd.caddr;
+    case 13: return nd.cval;
+    case 14:
+        return (nd.cst & 3u) | (((nd.cst >> 2) & 3u) << 8) | (((nd.cst >> 4) & 3u) << 16) |
+               (((nd.cst >> 6) & 3u) << 24);
+    default: return (nd.ctl & 0xFFu) | (flags << 8) | (nd.ip << 16);
+    }
 }
 template <int NW>
-DEVI uint64_t hash_rec(uint32_t node, const uint32_t (&w)[16]) {
+DEVI uint64_t node_hash(uint32_t node, const Node &nd, uint32_t flags) {
     uint64_t h = 0x9E3779B97F4A7C15ULL * (uint64_t)(node + 1);
 #pragma unroll
-    for (int i = 0; i < NW; ++i) h = fmix64(h ^ ((uint64_t)w[i] | ((uint64_t)i << 32)));
+    for (int i = 0; i < NW; ++i) h = fmix64(h ^ ((uint64_t)rec_word(nd, flags, i) | ((uint64_t)i << 32)));
     return h;
 }
-DEVI void store_rec(dsm_node_state *dst, const uint32_t (&w)[16]) {
+DEVI void store_rec(dsm_node_state *dst, const Node &nd, uint32_t flags) {
     uint4 *p = reinterpret_cast<uint4 *>(dst);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) p[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    for (int k = 0; k < 4; ++k)
+        p[k] = make_uint4(rec_word(nd, flags, 4 * k), rec_word(nd, flags, 4 * k + 1),
+                          rec_word(nd, flags, 4 * k + 2), rec_word(nd, flags, 4 * k + 3));
 }
 
 template <int NP>
@@ -234,15 +243,19 @@ DEVI void start_system(Node &nd, uint32_t (&cur)[4], uint32_t (&nxt)[4], const u
     }
 }
 
-/* ---- the transition kernel ------------------------------------------------------------ */
+/* ---- the transition kernel ------------------------------------------------------------ *
+ * One loop iteration = one lock-step round of every system resident in the wave.  The
+ * 13 message handlers + 2 issue paths are evaluated as ONE predicated data flow (a shared
+ * decode, per-type predicates, selects): a divergent 17-way switch costs every wave the sum
+ * of the taken cases plus their exec-mask bookkeeping, this costs one straight line.  Only
+ * the once-per-node dump and the trace-chunk refill are real branches.                    */
 template <int NP, int RING, int WAVES, bool GEN>
 __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
     constexpr int GPW = 64 / NP;
     constexpr uint32_t NPM = (1u << NP) - 1u;
-    constexpr uint64_t SPAT = (NP == 8) ? 0x0101010101010101ull : 0x1111111111111111ull;
 
-    __shared__ uint32_t s_ring[WAVES][RING][64];
-    __shared__ uint2 s_out[WAVES][64];
+    __shared__ uint32_t s_ring[WAVES][RING][64];                     /* inbox rings      */
+    __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][128]; /* 2 words / lane */
     __shared__ unsigned long long s_cnt[WAVES][K_N];
 
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -259,7 +272,7 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
     const uint16_t *tb = nullptr;
     uint64_t sys = 0;
-    uint32_t rounds = 0;
+    uint32_t rounds = 0, rmsg = 0;
     bool live = false;
     nd.ctl = 0; nd.ip = 0; nd.nins = 0; nd.rh = 0; nd.dh = 0;
 #pragma unroll
@@ -274,209 +287,145 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
     for (;;) {
         if (__ballot(live) == 0) break;
 
-        /* ---- (1) this round's action, from state at the start of the round ---- */
+        /* ---- (1) this round's action, from state at the start of the round ---------- */
         const uint32_t cnt0 = nd.rh >> 8, head0 = nd.rh & 0xFFu;
-        const uint32_t rmsg = s_ring[wv][head0][lane];
-        uint32_t op = OP_IDLE, w = 0;
-        if (live) {
-            if (cnt0) {                                               /* drain :158-169 */
-                w = rmsg;
-                op = w & 15u;
-                nd.rh = ((head0 + 1) & (RING - 1)) | ((cnt0 - 1) << 8);
-            } else if (!(nd.ctl & C_WAIT)) {                          /* :578-581 */
-                if (nd.ip < nd.nins) {                                /* :590-592 */
-                    uint32_t ins;
-                    if (GEN) {
-                        ins = gen_instr<NP>(A.seed, A.dist, A.first_sys + sys, node, nd.ip);
-                    } else {
-                        const uint32_t k = nd.ip & 7u, d = sel4(cur, k >> 1);
-                        ins = (k & 1u) ? (d >> 16) : (d & 0xFFFFu);
-                    }
-                    op = (ins >> 15) ? OP_WR : OP_RD;
-                    w = op | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
-                    nd.ip++;
-                    if (!GEN && (nd.ip & 7u) == 0 && nd.ip < nd.nins) {
+        const bool hasMsg = live && cnt0 != 0;                            /* :158-169 */
+        const bool canIssue = live && !hasMsg && !(nd.ctl & C_WAIT);      /* :578-581 */
+        const bool doIssue = canIssue && nd.ip < nd.nins;                 /* :590-592 */
+        const bool doDump = canIssue && !doIssue && !(nd.ctl & C_DUMPED); /* :688-697 */
+        nd.rh = hasMsg ? (((head0 + 1) & (RING - 1)) | ((cnt0 - 1) << 8)) : nd.rh;
+        uint32_t w = rmsg, op = rmsg & 15u;
+        if (doIssue) {
+            uint32_t ins;
+            if (GEN) {
+                ins = gen_instr<NP>(A.seed, A.dist, A.first_sys + sys, node, nd.ip);
+            } else {
+                const uint32_t k = nd.ip & 7u, d = sel4(cur, k >> 1);
+                ins = (k & 1u) ? (d >> 16) : (d & 0xFFFFu);
+            }
+            op = (ins >> 15) ? OP_WR : OP_RD;
+            w = op | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
+            nd.ip++;
+            if (!GEN && (nd.ip & 7u) == 0 && nd.ip < nd.nins) {           /* next chunk */
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-                        if (nd.ip + 8 < nd.nins) {
-                            const uint4 v = ld16(tb + nd.ip + 8);
-                            nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
-                        }
-                    }
-                } else if (!(nd.ctl & C_DUMPED)) {                    /* :688-697 */
-                    op = OP_DUMP;
+                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+                if (nd.ip + 8 < nd.nins) {
+                    const uint4 v = ld16(tb + nd.ip + 8);
+                    nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
                 }
             }
         }
+        op = hasMsg ? op : doIssue ? op : doDump ? OP_DUMP : OP_IDLE;
 
-        /* ---- (2) decode + read the line / directory entry / memory byte it touches ---- */
+        /* ---- (2) decode + the line / directory entry / memory byte it touches -------- */
         const uint32_t a = (w >> 4) & 0x7Fu, v = (w >> 11) & 0xFFu, r2 = (w >> 19) & 7u;
         const uint32_t excl = (w >> 22) & 1u, s = (w >> 23) & 7u;
-        const uint32_t H = a >> 4, blk = a & 15u, idx = a & 3u;        /* :177-184 */
+        const uint32_t H = a >> 4, blk = a & 15u, idx = a & 3u;          /* :177-184 */
         const uint32_t La = get8(nd.caddr, idx), Lv = get8(nd.cval, idx), Ls = get2(nd.cst, idx);
         const uint32_t Db = getb16(nd.bv, blk), Ds = get2(nd.dst, blk), Mv = getb16(nd.mem, blk);
-        const bool home = (H == node);
-        uint32_t nLa = La, nLv = Lv, nLs = Ls, nDb = Db, nDs = Ds, nMv = Mv;
-        uint32_t o0 = 0, o1 = 0;
-        bool evict = false;
+        const uint32_t pend = nd.ctl & 0xFFu;
+
+        const bool tRREQ = op == T_RREQ, tWREQ = op == T_WREQ, tRRD = op == T_RRD;
+        const bool tRWR = op == T_RWR, tRID = op == T_RID, tINV = op == T_INV;
+        const bool tUPG = op == T_UPG, tWBINV = op == T_WBINV, tWBINT = op == T_WBINT;
+        const bool tFLUSH = op == T_FLUSH, tFLINV = op == T_FLINV, tEVS = op == T_EVS;
+        const bool tEVM = op == T_EVM, tRD = op == OP_RD, tWR = op == OP_WR;
+
+        const bool home = (H == node), atR2 = (node == r2);
+        const bool hit = (La == a), valid = (Ls != CI), hitv = hit && valid;
+        const bool mOrE = (Ls <= CE);
         const uint32_t sbit = 1u << s;
+        const bool sSet = (Db & sbit) != 0u;
+        const uint32_t ob = Db & NPM;
+        const uint32_t own = __builtin_ctz(ob | 0x80000000u);            /* findOwner :98 */
+        const bool fwd = (Ds == DEM) && (own != s);      /* owner elsewhere: forward */
 
-        /* ---- (3) the transition ---- */
-        switch (op) {
-        case T_RREQ:                                                   /* :188-236 */
-            if (!home) { nd.ctl |= C_ASSERT; break; }
-            if (Ds == DU) {
-                nDs = DEM; nDb = sbit;
-                o0 = to(mbody(T_RRD, a, Mv, 0, 1), s);
-            } else if (Ds == DS) {
-                nDb = Db | sbit;
-                o0 = to(mbody(T_RRD, a, Mv, 0, 0), s);
-            } else {
-                const uint32_t ob = Db & NPM;
-                if (!ob) { nd.ctl |= C_ASSERT; break; }               /* :213 */
-                const uint32_t own = __builtin_ctz(ob);
-                if (own == s) {
-                    o0 = to(mbody(T_RRD, a, Mv, 0, 1), s);
-                } else {
-                    o0 = to(mbody(T_WBINT, a, 0, s), own);
-                    nDs = DS; nDb = Db | sbit;
-                }
-            }
-            break;
-        case T_RRD:                                                    /* :238-247 */
-            evict = (La != 0xFFu && La != a && Ls != CI);
-            nLa = a; nLv = v; nLs = excl ? CE : CS;
-            nd.ctl &= ~C_WAIT;
-            break;
-        case T_WBINT:                                                  /* :249-271 */
-            if (La == a && (Ls == CM || Ls == CE)) {
-                o0 = mbody(T_FLUSH, a, Lv, r2) | (1u << (24 + H)) | (1u << (24 + r2));
-                nLs = CS;
-            }
-            break;
-        case T_FLUSH:                                                  /* :273-296 */
-            if (home) nMv = v;
-            if (node == r2) {
-                evict = (La != 0xFFu && La != a && Ls != CI);
-                nLa = a; nLv = v; nLs = CS;
-                nd.ctl &= ~C_WAIT;
-            }
-            break;
-        case T_UPG:                                                    /* :298-328 */
-            if (!home) { nd.ctl |= C_ASSERT; break; }
-            o0 = to(mbody(T_RID, a, (Ds == DS) ? (Db & ~sbit & 0xFFu) : 0u), s);
-            nDs = DEM; nDb = sbit;
-            break;
-        case T_RID:                                                    /* :330-364 */
-            if (La == a) {
-                if (Ls != CM) { nLv = nd.ctl & 0xFFu; nLs = CM; }
-                const uint32_t m = v & NPM & ~(1u << node);
-                if (m) o0 = mbody(T_INV, a) | (m << 24);
-            }
-            nd.ctl &= ~C_WAIT;
-            break;
-        case T_INV:                                                    /* :366-373 */
-            if (La == a && (Ls == CS || Ls == CE)) nLs = CI;
-            break;
-        case T_WREQ:                                                   /* :375-435 */
-            if (!home) { nd.ctl |= C_ASSERT; break; }
-            nMv = v;                                                   /* :379 */
-            if (Ds == DU) {
-                nDs = DEM; nDb = sbit;
-                o0 = to(mbody(T_RWR, a), s);
-            } else if (Ds == DS) {
-                o0 = to(mbody(T_RID, a, Db & ~sbit & 0xFFu), s);
-                nDs = DEM; nDb = sbit;
-            } else {
-                const uint32_t ob = Db & NPM;
-                if (!ob) { nd.ctl |= C_ASSERT; break; }               /* :408 */
-                const uint32_t own = __builtin_ctz(ob);
-                if (own == s) {
-                    o0 = to(mbody(T_RWR, a), s);
-                } else {
-                    o0 = to(mbody(T_WBINV, a, 0, s), own);
-                    nDb = sbit;
-                }
-            }
-            break;
-        case T_RWR:                                                    /* :437-449 */
-            if (!(La == a || La == 0xFFu || Ls == CI)) { nd.ctl |= C_ASSERT; break; } /* :443 */
-            nLa = a; nLv = nd.ctl & 0xFFu; nLs = CM;
-            nd.ctl &= ~C_WAIT;
-            break;
-        case T_WBINV:                                                  /* :451-473 */
-            if (La == a && (Ls == CM || Ls == CE)) {
-                o0 = mbody(T_FLINV, a, Lv, r2) | (1u << (24 + H)) | (1u << (24 + r2));
-                nLs = CI;
-            }
-            break;
-        case T_FLINV:                                                  /* :475-496 */
-            if (home) { nMv = v; nDs = DEM; nDb = 1u << r2; }
-            if (node == r2) {
-                if (!(La == a || La == 0xFFu || Ls == CI)) { nd.ctl |= C_ASSERT; break; } /* :489 */
-                nLa = a; nLv = v; nLs = CM;
-                nd.ctl &= ~C_WAIT;
-            }
-            break;
-        case T_EVS:                                                    /* :498-539 */
-            if (home) {
-                if (Db & sbit) {
-                    nDb = Db & ~sbit;
-                    const uint32_t rem = __builtin_popcount(nDb & NPM);
-                    if (rem == 0) {
-                        nDs = DU;
-                    } else if (rem == 1 && Ds == DS) {
-                        nDs = DEM;
-                        o0 = to(mbody(T_EVS, a), __builtin_ctz(nDb & NPM));
-                    }
-                }
-            } else if (s == H && La == a && Ls == CS) {
-                nLs = CE;
-            }
-            break;
-        case T_EVM:                                                    /* :541-561 */
-            if (!home) { nd.ctl |= C_ASSERT; break; }
-            nMv = v;
-            if (Ds == DEM && (Db & sbit)) { nDb = 0; nDs = DU; }
-            break;
-        case OP_RD:                                                    /* :607-630 */
-            if (H >= (uint32_t)NP) { nd.ctl |= C_ASSERT; break; }
-            if (!(La == a && Ls != CI)) {
-                evict = (La != 0xFFu && Ls != CI);
-                o1 = to(mbody(T_RREQ, a), H);
-                nd.ctl |= C_WAIT;
-                nLa = a; nLv = 0; nLs = CI;
-            }
-            break;
-        case OP_WR:                                                    /* :632-685 */
-            if (H >= (uint32_t)NP) { nd.ctl |= C_ASSERT; break; }
-            nd.ctl = (nd.ctl & ~0xFFu) | v;                            /* :633 */
-            if (La == a && Ls != CI) {
-                nLv = v; nLs = CM;                                     /* :640-659 */
-                if (Ls == CS) { o1 = to(mbody(T_UPG, a), H); nd.ctl |= C_WAIT; }
-            } else {
-                evict = (La != 0xFFu && Ls != CI);
-                o1 = to(mbody(T_WREQ, a, v), H);
-                nd.ctl |= C_WAIT;
-                nLa = a; nLv = 0; nLs = CI;
-            }
-            break;
-        case OP_DUMP: {                                                /* :688-697 */
-            nd.ctl |= C_DUMPED;
-            uint32_t rw[16];
-            build_rec(nd, 2u, rw);
-            nd.dh = hash_rec<15>(node, rw);
-            if (A.snap) store_rec(&A.snap_dump[sys * NP + node], rw);
-            break;
-        }
-        default:
-            break;
-        }
-        /* handleCacheReplacement :742-773 -- the victim goes first in program order */
-        if (evict)
-            o0 = to((Ls == CM) ? mbody(T_EVM, La, Lv) : mbody(T_EVS, La), La >> 4);
+        /* reference asserts (:189-190,:213,:299-300,:376-377,:408,:443,:489,:542-543) */
+        const bool lineOK = hit || La == 0xFFu || !valid;
+        const bool emNoOwner = (Ds == DEM) && ob == 0u;
+        const bool issueBad = (tRD || tWR) && H >= (uint32_t)NP;
+        const bool asrt = ((tRREQ || tWREQ || tUPG || tEVM) && !home) ||
+                          ((tRREQ || tWREQ) && emNoOwner) || (tRWR && !lineOK) ||
+                          (tFLINV && atR2 && !lineOK) || issueBad;
+        const bool rreq = tRREQ && home && !emNoOwner;
+        const bool wreq = tWREQ && home && !emNoOwner;
+        const bool upg = tUPG && home;
 
-        /* ---- (4) write back ---- */
+        /* memory: WRITE_REQUEST :379, FLUSH :276, FLUSH_INVACK :478, EVICT_MODIFIED :544 */
+        const uint32_t nMv = (home && (tWREQ || tFLUSH || tFLINV || tEVM)) ? v : Mv;
+
+        /* directory */
+        const uint32_t evDb = Db & ~sbit;
+        const uint32_t rem = __builtin_popcount(evDb & NPM);
+        const bool evsH = tEVS && home && sSet;                           /* :501-521 */
+        uint32_t nDb = Db, nDs = Ds;
+        nDb = rreq ? ((Ds == DU) ? sbit : (Db | sbit)) : nDb;            /* :196-234 */
+        nDs = rreq ? (((Ds == DU) || (Ds == DEM && !fwd)) ? DEM : DS) : nDs;
+        nDb = (wreq || upg) ? sbit : nDb;                                /* :381-433, :302-327 */
+        nDs = (wreq || upg) ? DEM : nDs;
+        nDb = (tFLINV && home) ? (1u << r2) : nDb;                       /* :479-480 */
+        nDs = (tFLINV && home) ? DEM : nDs;
+        nDb = evsH ? evDb : nDb;
+        nDs = evsH ? ((rem == 0) ? DU : (rem == 1 && Ds == DS) ? DEM : Ds) : nDs;
+        const bool evmClr = tEVM && home && Ds == DEM && sSet;            /* :545-547 */
+        nDb = evmClr ? 0u : nDb;
+        nDs = evmClr ? DU : nDs;
+
+        /* sends: o0 = victim / reply / forward / flush / INV fan-out, o1 = request */
+        uint32_t o0 = 0;
+        o0 = rreq ? (fwd ? to(mbody(T_WBINT, a, 0, s), own)
+                         : to(mbody(T_RRD, a, Mv, 0, Ds != DS ? 1u : 0u), s)) : o0;
+        o0 = wreq ? (fwd ? to(mbody(T_WBINV, a, 0, s), own)
+                         : (Ds == DS) ? to(mbody(T_RID, a, Db & ~sbit & 0xFFu), s)
+                                      : to(mbody(T_RWR, a), s)) : o0;
+        o0 = upg ? to(mbody(T_RID, a, (Ds == DS) ? (Db & ~sbit & 0xFFu) : 0u), s) : o0;
+        o0 = (evsH && rem == 1 && Ds == DS)
+                 ? to(mbody(T_EVS, a), __builtin_ctz((evDb & NPM) | 0x80000000u)) : o0;
+        const bool flushOut = (tWBINT || tWBINV) && hit && mOrE;          /* :251-264, :453-466 */
+        o0 = flushOut ? (mbody(tWBINT ? T_FLUSH : T_FLINV, a, Lv, r2) | (1u << (24 + H)) |
+                         (1u << (24 + r2))) : o0;
+        const uint32_t invm = v & NPM & ~(1u << node);                   /* :350-362 */
+        o0 = (tRID && hit && invm) ? (mbody(T_INV, a) | (invm << 24)) : o0;
+        const bool isIssue = (tRD || tWR) && !issueBad;
+        const bool installRd = tRRD || (tFLUSH && atR2);                 /* :238-247, :286-295 */
+        const bool evict = (La != 0xFFu) && valid &&                      /* :742-773 */
+                           ((installRd && !hit) || (isIssue && !hitv));
+        o0 = evict ? to((Ls == CM) ? mbody(T_EVM, La, Lv) : mbody(T_EVS, La), La >> 4) : o0;
+        const bool sendReq = isIssue && (!hitv || (tWR && Ls == CS));     /* :612-629, :646-684 */
+        const uint32_t o1 = sendReq ? to(mbody(tRD ? T_RREQ : (hitv ? T_UPG : T_WREQ), a,
+                                                (tWR && !hitv) ? v : 0u), H) : 0u;
+
+        /* cache line */
+        const bool installWr = (tRWR || (tFLINV && atR2)) && lineOK;      /* :437-449, :483-495 */
+        const bool issueMiss = isIssue && !hitv;
+        const bool wrHit = tWR && !issueBad && hitv;                      /* :640-659 */
+        const bool ridUp = tRID && hit && Ls != CM;                       /* :332-336 */
+        const uint32_t nLa = (installRd || installWr || issueMiss) ? a : La;
+        uint32_t nLv = Lv;
+        nLv = ridUp ? pend : nLv;
+        nLv = wrHit ? v : nLv;
+        nLv = issueMiss ? 0u : nLv;
+        nLv = installWr ? (tRWR ? pend : v) : nLv;
+        nLv = installRd ? v : nLv;
+        uint32_t nLs = Ls;
+        nLs = (tEVS && !home && s == H && hit && Ls == CS) ? CE : nLs;    /* :526-532 */
+        nLs = (tINV && hit && (Ls == CS || Ls == CE)) ? CI : nLs;         /* :366-373 */
+        nLs = flushOut ? (tWBINT ? CS : CI) : nLs;
+        nLs = ridUp ? CM : nLs;
+        nLs = wrHit ? CM : nLs;
+        nLs = issueMiss ? CI : nLs;
+        nLs = installWr ? CM : nLs;
+        nLs = installRd ? ((tRRD && excl) ? CE : CS) : nLs;
+
+        /* waitingForReply / pendingWriteValue / assert flag */
+        const bool clrWait = installRd || installWr || tRID;
+        uint32_t ctl = nd.ctl;
+        ctl = sendReq ? (ctl | C_WAIT) : clrWait ? (ctl & ~C_WAIT) : ctl;
+        ctl = (tWR && !issueBad) ? ((ctl & ~0xFFu) | v) : ctl;           /* :633 */
+        ctl = asrt ? (ctl | C_ASSERT) : ctl;
+        nd.ctl = ctl;
+
+        /* ---- (3) write back (idle lanes rewrite unchanged values) ------------------- */
         nd.caddr = set8(nd.caddr, idx, nLa);
         nd.cval = set8(nd.cval, idx, nLv);
         nd.cst = set2(nd.cst, idx, nLs);
@@ -488,66 +437,73 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
 #pragma unroll
             for (uint32_t k = 0; k < 7; ++k) nd.tc[k] += (q == k) ? inc : 0u;
         }
+        if (doDump) {                                                    /* :688-697 */
+            nd.ctl |= C_DUMPED;
+            nd.dh = node_hash<15>(node, nd, 2u);
+            if (A.snap) store_rec(&A.snap_dump[sys * NP + node], nd, 2u);
+        }
 
-        /* ---- (5) end-of-round delivery: ascending sender, then program order ---- */
+        /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        s_out[wv][lane] = make_uint2(o0, o1);
+        reinterpret_cast<uint2 *>(s_out[wv])[lane] = make_uint2(o0, o1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint64_t sendb = __ballot((o0 | o1) != 0u);
-        if (sendb) {
-            uint32_t hh = nd.rh & 0xFFu, cc = nd.rh >> 8;
-            bool ovf = false;
+        uint32_t R = 0;                  /* bit 2*sender+word: that word is addressed to me */
+        {
+            const uint4 *g = reinterpret_cast<const uint4 *>(&s_out[wv][2 * gbase]);
 #pragma unroll
-            for (uint32_t si = 0; si < (uint32_t)NP; ++si) {
-                if (sendb & (SPAT << si)) {
-                    const uint2 x = s_out[wv][gbase + si];
-                    if ((x.x >> (24 + node)) & 1u) {
-                        if (cc < (uint32_t)RING) {
-                            s_ring[wv][(hh + cc) & (RING - 1)][lane] = (x.x & 0x7FFFFFu) | (si << 23);
-                            ++cc;
-                        } else {
-                            ovf = true;
-                        }
-                    }
-                    if ((x.y >> (24 + node)) & 1u) {
-                        if (cc < (uint32_t)RING) {
-                            s_ring[wv][(hh + cc) & (RING - 1)][lane] = (x.y & 0x7FFFFFu) | (si << 23);
-                            ++cc;
-                        } else {
-                            ovf = true;
-                        }
-                    }
+            for (int q = 0; q < NP / 2; ++q) {
+                const uint4 x = g[q];
+                R |= (__builtin_amdgcn_ubfe(x.x, 24 + node, 1) << (4 * q)) |
+                     (__builtin_amdgcn_ubfe(x.y, 24 + node, 1) << (4 * q + 1)) |
+                     (__builtin_amdgcn_ubfe(x.z, 24 + node, 1) << (4 * q + 2)) |
+                     (__builtin_amdgcn_ubfe(x.w, 24 + node, 1) << (4 * q + 3));
+            }
+        }
+        {
+            const uint32_t hh = nd.rh & 0xFFu;
+            uint32_t cc = nd.rh >> 8;
+            bool ovf = false;
+            while (R) {
+                const uint32_t j = __builtin_ctz(R);
+                R &= R - 1;
+                const uint32_t x = s_out[wv][2 * gbase + j];
+                if (cc < (uint32_t)RING) {
+                    s_ring[wv][(hh + cc) & (RING - 1)][lane] = (x & 0x7FFFFFu) | ((j >> 1) << 23);
+                    ++cc;
+                } else {
+                    ovf = true;
                 }
             }
             nd.rh = hh | (cc << 8);
             if (ovf) nd.ctl |= C_OVF;
+            rmsg = s_ring[wv][hh][lane];          /* next round's head, prefetched */
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 
-        /* ---- (6) per-system termination (Appendix A step 4) ---- */
-        const uint64_t actb = __ballot(live && op != OP_IDLE);
-        const uint64_t asrb = __ballot(live && (nd.ctl & C_ASSERT));
-        const uint64_t ovfb = __ballot(live && (nd.ctl & C_OVF));
+        /* ---- (5) per-system termination (Appendix A step 4) -------------------------- */
+        const uint64_t actb = __ballot(op != OP_IDLE);
+        const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
         const uint32_t gact = (uint32_t)(actb >> gbase) & NPM;
-        const bool gasr = ((asrb >> gbase) & NPM) != 0, govf = ((ovfb >> gbase) & NPM) != 0;
+        const bool gbad = ((badb >> gbase) & NPM) != 0;
         if (live && gact) ++rounds;
-        const bool done = live && (gact == 0 || gasr || govf || rounds >= DSM_MAX_ROUNDS);
+        const bool done = live && (gact == 0 || gbad || rounds >= DSM_MAX_ROUNDS);
 
         const uint64_t doneb = __ballot(done);
         if (doneb) {
             const uint64_t dumpb = __ballot((nd.ctl & C_DUMPED) != 0u);
+            const uint64_t asrb = __ballot((nd.ctl & C_ASSERT) != 0u);
             if (done) {
                 const uint32_t dmask = (uint32_t)(dumpb >> gbase) & NPM;
+                const bool gasr = ((asrb >> gbase) & NPM) != 0;
                 uint32_t st;
                 if (gasr) st = DSM_ASSERT_FAILED;
-                else if (govf) st = DSM_RING_OVERFLOW;
+                else if (gbad) st = DSM_RING_OVERFLOW;
                 else if (gact == 0) st = (dmask == NPM) ? DSM_COMPLETED : DSM_DEADLOCKED;
                 else st = DSM_ROUND_LIMIT;
                 const bool handoff = (st == DSM_RING_OVERFLOW) && A.ovf_list;
-                uint32_t rw[16];
-                build_rec(nd, ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u), rw);
-                uint64_t fh = hash_rec<16>(node, rw);
-                if (A.snap && !handoff) store_rec(&A.snap_final[sys * NP + node], rw);
+                const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
+                uint64_t fh = node_hash<16>(node, nd, fl);
+                if (A.snap && !handoff) store_rec(&A.snap_final[sys * NP + node], nd, fl);
                 fh = gsum64<NP>(fh);
                 const uint64_t dh = gsum64<NP>(nd.dh);
                 const uint32_t ins = gsum32<NP>(nd.ip);
@@ -638,30 +594,45 @@ __global__ void __launch_bounds__(256) reduce_kernel(const unsigned long long *p
     }
 }
 
-/* ---- trace generator: one thread = one 16-byte chunk (8 instructions) ----------------- */
+/* ---- trace generator ------------------------------------------------------------------
+ * One workgroup iteration = one (system, node) slot of `stride` instructions; each lane
+ * produces 16-byte chunks (8 instructions) and streams them out with non-temporal stores
+ * (written once, read later by a different kernel).  No 64-bit divisions in the index math. */
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 template <int NP>
 __global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist, uint64_t first,
                                                   uint64_t n_sys, uint32_t n_instr,
                                                   uint32_t stride, uint16_t *traces,
                                                   uint32_t *counts) {
-    const uint32_t cps = stride / 8;                 /* chunks per node slot */
-    const uint64_t total = n_sys * NP * (uint64_t)cps;
-    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total;
-         c += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t slot = c / cps;
-        const uint32_t k = (uint32_t)(c - slot * cps);
+    const uint32_t cps = stride >> 3;                /* 16-byte chunks per node slot */
+    const uint64_t nslots = n_sys * NP;
+    const uint64_t gmul = seed * 0x9E3779B97F4A7C15ULL;
+    for (uint64_t slot = blockIdx.x; slot < nslots; slot += gridDim.x) {
         const uint64_t sys = slot / NP;
-        const uint32_t node = (uint32_t)(slot - sys * NP);
-        uint32_t d[4];
+        const uint32_t node = (uint32_t)(slot % NP);
+        /* key = (sys << 16) | (node << 12) | (idx >> 2) -- disjoint fields, so + == | */
+        const uint64_t base = gmul + ((first + sys) << 16) + ((uint64_t)node << 12);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(traces + slot * stride);
+        for (uint32_t k = threadIdx.x; k < cps; k += blockDim.x) {
+            u32x4 v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t i0 = k * 8 + 2 * j;
-            const uint32_t lo = (i0 < n_instr) ? gen_instr<NP>(seed, dist, first + sys, node, i0) : 0u;
-            const uint32_t hi = (i0 + 1 < n_instr) ? gen_instr<NP>(seed, dist, first + sys, node, i0 + 1) : 0u;
-            d[j] = lo | (hi << 16);
+            for (int half = 0; half < 2; ++half) {
+                const uint32_t i0 = k * 8 + 4 * half;               /* 4 instructions */
+                const uint64_t r = splitmix(base + (i0 >> 2));
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const uint32_t ia = i0 + 2 * j;
+                    const uint32_t lo = (ia < n_instr)
+                        ? instr_from_bits<NP>((uint32_t)(r >> (32 * j)) & 0xFFFFu, dist) : 0u;
+                    const uint32_t hi = (ia + 1 < n_instr)
+                        ? instr_from_bits<NP>((uint32_t)(r >> (32 * j + 16)) & 0xFFFFu, dist) : 0u;
+                    v[2 * half + j] = lo | (hi << 16);
+                }
+            }
+            __builtin_nontemporal_store(v, dst + k);
         }
-        reinterpret_cast<uint4 *>(traces)[c] = make_uint4(d[0], d[1], d[2], d[3]);
-        if (k == 0 && counts) counts[slot] = n_instr;
+        if (threadIdx.x == 0 && counts) counts[slot] = n_instr;
     }
 }
 
@@ -947,9 +918,8 @@ extern "C" int dsm_generate_device(dsm_ctx *c, const dsm_gen *g, uint64_t first_
     if (g->n_instr > c->cfg.max_instr || g->dist < 0 || g->dist > 2) return DSM_E_INVAL;
     if (n_sys == 0) return DSM_OK;
     HIPCK(hipSetDevice(c->device));
-    const uint64_t chunks = n_sys * (uint64_t)c->cfg.np * (c->cfg.max_instr / 8);
-    uint64_t blocks = (chunks + 255) / 256;
-    const uint64_t cap = (uint64_t)c->cus * 32;
+    uint64_t blocks = n_sys * (uint64_t)c->cfg.np;
+    const uint64_t cap = (uint64_t)c->cus * 16;
     if (blocks > cap) blocks = cap;
     if (c->cfg.np == 4)
         hipLaunchKernelGGL(gen_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,

@@ -64,6 +64,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} not built (run `make -C hp-assignment-2_amd`)")
+        # torch (ROCm build) bundles its own libamdhip64.so.7 / libhsa-runtime64.so.1.  A
+        # process must hold ONE HIP runtime: load torch's first so libdsm's DT_NEEDED entries
+        # (same sonames) bind to it and device pointers / streams are shared with torch.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
         sig = {

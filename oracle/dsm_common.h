@@ -85,8 +85,10 @@ static inline uint64_t dsm_hash_rec(int node, const dsm_rec *r, int nwords) {
 
 /* Counter-based synthetic trace generator.  Instruction idx of node `node`
  * of system `sys` depends only on (seed, dist, np, sys, node, idx): results are independent
- * of how systems are batched or sharded over GPUs.  Packed u16:
- *   bit 15 = WR, bits 8..14 = address (7 bits), bits 0..7 = value (0 for RD, :810). */
+ * of how systems are batched or sharded over GPUs.  One splitmix64 output feeds 4
+ * consecutive instructions (16 bits each: bit 0 WR, bits 1-8 value, bits 9-15 address
+ * selector).  Packed u16: bit 15 = WR, bits 8..14 = address (7 bits), bits 0..7 = value
+ * (0 for RD, :810). */
 static inline uint64_t dsm_splitmix(uint64_t z) {
     z += 0x9E3779B97F4A7C15ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -95,15 +97,16 @@ static inline uint64_t dsm_splitmix(uint64_t z) {
 }
 static inline uint16_t dsm_gen_instr(uint64_t seed, int dist, int np, uint64_t sys, int node,
                                      uint32_t idx) {
-    uint64_t key = (sys << 16) | ((uint64_t)node << 12) | (uint64_t)(idx & 0xFFF);
+    uint64_t key = (sys << 16) | ((uint64_t)node << 12) | (uint64_t)((idx & 0xFFF) >> 2);
     uint64_t r = dsm_splitmix(seed * 0x9E3779B97F4A7C15ULL + key);
-    uint32_t wr = (uint32_t)(r & 1);
-    uint32_t val = wr ? (uint32_t)((r >> 8) & 0xFF) : 0;
-    uint32_t sel = (uint32_t)(r >> 32);
+    uint32_t h = (uint32_t)(r >> (16 * (idx & 3))) & 0xFFFF;
+    uint32_t wr = h & 1;
+    uint32_t val = wr ? (h >> 1) & 0xFF : 0;
+    uint32_t sel = h >> 9;
     uint32_t addr;
-    if (dist == DIST_HOT) addr = (sel & 3) * 0x11;              /* {0x00,0x11,0x22,0x33} */
+    if (dist == DIST_HOT) addr = (sel & 3) * 0x11;                       /* {0x00,0x11,0x22,0x33} */
     else if (dist == DIST_EVICT) addr = (sel & (uint32_t)(np * 4 - 1)) * 4; /* a%4==0 */
-    else addr = sel & (uint32_t)(np * 16 - 1);                  /* uniform 0..np*16-1 */
+    else addr = sel & (uint32_t)(np * 16 - 1);                           /* uniform 0..np*16-1 */
     return (uint16_t)((wr << 15) | (addr << 8) | val);
 }
 
