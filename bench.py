@@ -226,7 +226,7 @@ def main():
             "systems_per_s": round(c["systems"] * K / elapsed_max, 1),
             "instructions_per_s": round(c["instrs"] * K / elapsed_max, 1),
             "counters": {k: c[k] for k in ("msgs", "instrs", "rounds", "systems", "max_rounds",
-                                           "overflow_reruns", "status_COMPLETED",
+                                           "overflow_reruns", "wave_rounds", "status_COMPLETED",
                                            "status_DEADLOCKED")},
             "sum_final_hash": hex(c["sum_final_hash"]),
             "parity": parity,

@@ -9,17 +9,21 @@
  * lock-step schedule on an ensemble of independent systems.
  *
  * Mapping (one wave64 = 64/NP systems, one lane = one node):
- *   - node state lives in VGPRs, bit-packed: memory 4 dwords, directory bitVectors 4 dwords,
- *     directory states 2 bits x 16, cache address / value bytes, cache states 2 bits x 4;
- *   - inboxes are LDS rings s_ring[wave][slot][lane] (each lane touches only its own column:
- *     bank = lane % 32, conflict-free);
- *   - one round = every lane takes one action; sends go to a per-lane LDS outbox of two words
- *     (body + destination bitmask; the REPLY_ID INV fan-out is one word with a multi-bit mask),
- *     then each receiver lane appends the words addressed to it in ascending sender order,
- *     which is exactly the reference's (sender, program order) delivery order;
- *   - termination per system by wave ballot; finished systems are replaced from a sharded
- *     device work counter (persistent kernel), so lanes never idle on a long-tail system;
- *   - traces are read as 16-byte chunks per lane (cur + prefetched next) from HBM.
+ *   - per-node registers: directory states (2 bits x 16), cache addresses / values (one byte
+ *     per line), cache states (2 bits x 4), control word, counters;
+ *   - per-node LDS column s_mb[wave][block][lane] = memory byte | bitVector byte << 8, so a
+ *     message touches its home block with one ds_read_u16 / ds_write_b16 (bank = lane / 2,
+ *     conflict-free) instead of a runtime byte select over 8 registers;
+ *   - inboxes: LDS rings s_ring[wave][slot][lane] (bank = lane % 32, conflict-free);
+ *   - a round: every lane takes one action (predicated data flow, no per-type branches),
+ *     writes <= 2 outgoing words + their destination masks to LDS; each receiver gathers
+ *     the masks of its group with one ds_read_b128 and appends the words addressed to it in
+ *     ascending (sender, word) order -- the reference's (sender, program order) delivery;
+ *   - per-system termination by wave ballot; finished systems are replaced from sharded
+ *     device work counters (persistent kernel), so lanes never idle on a long-tail system;
+ *   - traces are read as 16-byte chunks per lane (current + prefetched next) from HBM;
+ *   - systems whose inbox would exceed the fast ring are re-run by the same kernel built
+ *     with the reference's 256-deep inbox, so results never depend on the fast ring size.
  */
 #include <hip/hip_runtime.h>
 
@@ -47,10 +51,14 @@ constexpr uint32_t C_WAIT = 1u << 8, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C_ASS
 
 /* counter slots (dsm_counters order) */
 enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
-       K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_N = 32 };
+       K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_N = 32 };
 
 constexpr uint64_t NO_SYS = ~0ull;
+constexpr int FB_RING = 256;        /* MSG_BUFFER_SIZE, assignment.c:12 */
 
+/* Kernel arguments live in device memory (not the kernarg segment): the hot loop needs
+ * almost none of them, and loads from a plain global pointer are not hoisted into SGPRs
+ * that would then stay live across the whole loop. */
 struct SimArgs {
     const uint16_t *traces;     /* [sys][np][stride] packed u16 (not GEN)                 */
     const uint32_t *counts;     /* [sys][np] (not GEN)                                     */
@@ -62,33 +70,20 @@ struct SimArgs {
     uint64_t first_sys;         /* GEN: global id of system index 0                        */
     uint64_t seed;
     int dist;
-    int snap;
-    dsm_sys_result *results;
-    dsm_node_state *snap_dump;
-    dsm_node_state *snap_final;
+    dsm_sys_result *results;    /* the transition kernel writes the first 16 bytes        */
+    uint4 *recs;                /* [sys][node][2] x 64 B: dump record, final record       */
     unsigned long long *partials;   /* [waves][K_N], written once per wave at exit         */
     unsigned int *claim;            /* 8 shard counters, 32 words apart                     */
-    uint32_t *ovf_list;             /* fast kernel: overflowing systems for the 256 re-run   */
+    uint32_t *ovf_list;             /* fast kernel: systems handed to the 256-deep re-run   */
     unsigned int *ovf_count;
 };
 
 /* ---- small bit-field helpers ------------------------------------------------------- */
-/* Runtime selection among 4 register words.  Written as masks on purpose: a ?: chain over
- * array elements gets folded into a runtime-indexed load, which sends the array to scratch. */
+/* Runtime selection among 4 register words, written as masks: a ?: chain over array
+ * elements gets folded into a runtime-indexed load, which sends the array to scratch. */
 DEVI uint32_t msk(bool b) { return 0u - (uint32_t)b; }
 DEVI uint32_t sel4(const uint32_t (&w)[4], uint32_t q) {
     return (w[0] & msk(q == 0)) | (w[1] & msk(q == 1)) | (w[2] & msk(q == 2)) | (w[3] & msk(q == 3));
-}
-DEVI uint32_t getb16(const uint32_t (&w)[4], uint32_t i) {
-    return __builtin_amdgcn_ubfe(sel4(w, i >> 2), (i & 3) * 8, 8);
-}
-DEVI void setb16(uint32_t (&w)[4], uint32_t i, uint32_t v) {
-    const uint32_t sh = (i & 3) * 8, q = i >> 2, m = 0xFFu << sh, x = v << sh;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t sel = msk(q == k) & m;
-        w[k] = (w[k] & ~sel) | (x & sel);
-    }
 }
 DEVI uint32_t get8(uint32_t w, uint32_t i) { return __builtin_amdgcn_ubfe(w, i * 8, 8); }
 DEVI uint32_t set8(uint32_t w, uint32_t i, uint32_t v) {
@@ -102,14 +97,14 @@ DEVI uint32_t set2(uint32_t w, uint32_t i, uint32_t v) {
 }
 
 /* message body: type[0:3] addr[4:10] payload[11:18] r2[19:21] excl[22];
- * ring entry = body | sender << 23; outbox entry = body | destination mask << 24 */
+ * ring entry = body | sender << 23; outbox word = body | destination mask << 24 */
 DEVI uint32_t mbody(uint32_t type, uint32_t addr, uint32_t payload = 0, uint32_t r2 = 0,
                     uint32_t excl = 0) {
     return type | (addr << 4) | (payload << 11) | (r2 << 19) | (excl << 22);
 }
 DEVI uint32_t to(uint32_t body, uint32_t dest) { return body | (1u << (24 + dest)); }
 
-/* ---- hashing / generator (same definitions as DESIGN.md; pinned by tests) ----------- */
+/* ---- hashing / generator (definitions in DESIGN.md; pinned by tests) ----------------- */
 DEVI uint64_t fmix64(uint64_t z) {
     z ^= z >> 33; z *= 0xff51afd7ed558ccdULL;
     z ^= z >> 33; z *= 0xc4ceb9fe1a85ec53ULL;
@@ -122,7 +117,7 @@ DEVI uint64_t splitmix(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
-/* One splitmix64 output feeds 4 consecutive instructions, 16 bits each (DESIGN.md). */
+/* One splitmix64 output feeds 4 consecutive instructions, 16 bits each. */
 template <int NP>
 DEVI uint32_t instr_from_bits(uint32_t h, int dist) {
     const uint32_t wr = h & 1u;
@@ -135,14 +130,13 @@ DEVI uint32_t instr_from_bits(uint32_t h, int dist) {
     return (wr << 15) | (addr << 8) | val;
 }
 template <int NP>
-DEVI uint32_t gen_instr(uint64_t seed, int dist, uint64_t sys, uint32_t node, uint32_t idx) {
+DEVI uint32_t gen_instr(uint64_t gmul, int dist, uint64_t sys, uint32_t node, uint32_t idx) {
     const uint64_t key = (sys << 16) | ((uint64_t)node << 12) | (uint64_t)((idx & 0xFFFu) >> 2);
-    const uint64_t r = splitmix(seed * 0x9E3779B97F4A7C15ULL + key);
+    const uint64_t r = splitmix(gmul + key);
     return instr_from_bits<NP>((uint32_t)(r >> (16 * (idx & 3u))) & 0xFFFFu, dist);
 }
 
 struct Node {
-    uint32_t mem[4], bv[4];
     uint32_t dst;     /* directory states, 2 bits per block                                 */
     uint32_t caddr;   /* cache addresses, one byte per line                                 */
     uint32_t cval;    /* cache values                                                       */
@@ -151,16 +145,13 @@ struct Node {
     uint32_t ip;      /* instructions issued                                                */
     uint32_t nins;    /* instructions in this node's trace                                  */
     uint32_t rh;      /* inbox head (bits 0-7) | count << 8                                 */
-    uint32_t tc[7];   /* messages handled by type, 16-bit fields (type t: tc[t/2], t%2)      */
-    uint64_t dh;      /* hash of the dump snapshot                                          */
+    uint32_t nmsg;    /* messages handled                                                   */
 };
 
-/* canonical 64-byte record (dsm_node_state) word i (i is a compile-time constant after
- * unrolling, so the switch folds away and no 16-register record is ever live) */
-DEVI uint32_t rec_word(const Node &nd, uint32_t flags, int i) {
+/* canonical 64-byte record (dsm_node_state) word i; mem / bv words come from LDS */
+DEVI uint32_t rec_word(const Node &nd, const uint32_t (&mb)[8], uint32_t flags, int i) {
     switch (i) {
-    case 0: case 1: case 2: case 3: return nd.mem[i];
-    case 4: case 5: case 6: case 7: return nd.bv[i - 4];
+    case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 7: return mb[i];
     case 8: case 9: case 10: case 11: {
         const uint32_t e = nd.dst >> (8 * (i - 8));
         return (e & 3u) | (((e >> 2) & 3u) << 8) | (((e >> 4) & 3u) << 16) | (((e >> 6) & 3u) << 24);
@@ -173,19 +164,31 @@ DEVI uint32_t rec_word(const Node &nd, uint32_t flags, int i) {
     default: return (nd.ctl & 0xFFu) | (flags << 8) | (nd.ip << 16);
     }
 }
-template <int NW>
-DEVI uint64_t node_hash(uint32_t node, const Node &nd, uint32_t flags) {
-    uint64_t h = 0x9E3779B97F4A7C15ULL * (uint64_t)(node + 1);
+/* memory (words 0-3) and bitVector (words 4-7) bytes of this lane's node, from LDS */
+template <int WAVES>
+DEVI void load_mb(const uint16_t (&smb)[WAVES][16][64], uint32_t wv, uint32_t lane,
+                  uint32_t (&mb)[8]) {
 #pragma unroll
-    for (int i = 0; i < NW; ++i) h = fmix64(h ^ ((uint64_t)rec_word(nd, flags, i) | ((uint64_t)i << 32)));
-    return h;
+    for (int k = 0; k < 8; ++k) mb[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t x = smb[wv][i][lane];
+        mb[i >> 2] |= (x & 0xFFu) << (8 * (i & 3));
+        mb[4 + (i >> 2)] |= (x >> 8) << (8 * (i & 3));
+    }
 }
-DEVI void store_rec(dsm_node_state *dst, const Node &nd, uint32_t flags) {
-    uint4 *p = reinterpret_cast<uint4 *>(dst);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        p[k] = make_uint4(rec_word(nd, flags, 4 * k), rec_word(nd, flags, 4 * k + 1),
-                          rec_word(nd, flags, 4 * k + 2), rec_word(nd, flags, 4 * k + 3));
+/* store this lane's 64-byte node record (dsm_node_state) */
+template <int WAVES>
+DEVI void store_rec(uint4 *dst, const Node &nd, const uint16_t (&smb)[WAVES][16][64],
+                    uint32_t wv, uint32_t lane, uint32_t flags) {
+    uint32_t mb[8];
+    load_mb<WAVES>(smb, wv, lane, mb);
+    dst[0] = make_uint4(mb[0], mb[1], mb[2], mb[3]);
+    dst[1] = make_uint4(mb[4], mb[5], mb[6], mb[7]);
+    dst[2] = make_uint4(rec_word(nd, mb, flags, 8), rec_word(nd, mb, flags, 9),
+                        rec_word(nd, mb, flags, 10), rec_word(nd, mb, flags, 11));
+    dst[3] = make_uint4(rec_word(nd, mb, flags, 12), rec_word(nd, mb, flags, 13),
+                        rec_word(nd, mb, flags, 14), rec_word(nd, mb, flags, 15));
 }
 
 template <int NP>
@@ -205,68 +208,45 @@ DEVI uint64_t gsum64(uint64_t x) {
 }
 DEVI uint4 ld16(const uint16_t *p) { return *reinterpret_cast<const uint4 *>(p); }
 
-template <int NP, bool GEN>
-DEVI void start_system(Node &nd, uint32_t (&cur)[4], uint32_t (&nxt)[4], const uint16_t *&tb,
-                       uint64_t sys, uint32_t node, const SimArgs &A) {
-    /* initializeProcessor :778-790 and main :142-146 */
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t b = 20u * node + 4u * k;
-        nd.mem[k] = (b & 0xFFu) | (((b + 1) & 0xFFu) << 8) | (((b + 2) & 0xFFu) << 16) |
-                    (((b + 3) & 0xFFu) << 24);
-        nd.bv[k] = 0;
-    }
-    nd.dst = 0xAAAAAAAAu;   /* all U */
-    nd.caddr = 0xFFFFFFFFu; /* address 0xFF */
-    nd.cval = 0;
-    nd.cst = 0xFFu;         /* all INVALID */
-    nd.ctl = 0;
-    nd.ip = 0;
-    nd.rh = 0;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) nd.tc[k] = 0;
-    nd.dh = 0;
-    if (GEN) {
-        nd.nins = A.n_instr;
-    } else {
-        const uint32_t c = A.counts[sys * NP + node];
-        nd.nins = c < A.stride ? c : A.stride;
-        tb = A.traces + (sys * NP + node) * (uint64_t)A.stride;
-        if (nd.nins > 0) {
-            const uint4 v = ld16(tb);
-            cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
-        }
-        if (nd.nins > 8) {
-            const uint4 v = ld16(tb + 8);
-            nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
-        }
-    }
+/* gather bit `r` of each of the 4 bytes of x into bits 0..3 */
+DEVI uint32_t gather4(uint32_t x, uint32_t r) {
+    const uint32_t t = (x >> r) & 0x01010101u;
+    return (t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu;
 }
 
 /* ---- the transition kernel ------------------------------------------------------------ *
- * One loop iteration = one lock-step round of every system resident in the wave.  The
- * 13 message handlers + 2 issue paths are evaluated as ONE predicated data flow (a shared
- * decode, per-type predicates, selects): a divergent 17-way switch costs every wave the sum
- * of the taken cases plus their exec-mask bookkeeping, this costs one straight line.  Only
- * the once-per-node dump and the trace-chunk refill are real branches.                    */
-template <int NP, int RING, int WAVES, bool GEN>
-__global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
+ * One loop iteration = one lock-step round of every system resident in the wave.  The 13
+ * message handlers + 2 issue paths are ONE predicated data flow (shared decode, per-type
+ * predicates, selects): a divergent 17-way switch costs every wave the sum of the taken
+ * cases plus their exec-mask bookkeeping.  Only the once-per-node dump, the trace-chunk
+ * refill and the per-system finish are real branches.                                   */
+template <int NP, int RING, int WAVES, bool GEN, bool TC, int OCC = 5>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
+sim_kernel(const SimArgs *Ap) {
     constexpr int GPW = 64 / NP;
     constexpr uint32_t NPM = (1u << NP) - 1u;
+    constexpr bool FB = (RING == FB_RING);   /* the 256-deep re-run kernel                */
+    /* TC: per-type message counters (DSM_F_TYPE_COUNTS), 16-bit fields per node and
+     * system, added to the wave counters when the system finishes (exact per system). */
 
-    __shared__ uint32_t s_ring[WAVES][RING][64];                     /* inbox rings      */
-    __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][128]; /* 2 words / lane */
+    __shared__ uint16_t s_mb[WAVES][16][64];                           /* mem | bv << 8 */
+    __shared__ uint32_t s_ring[WAVES][RING][64];                       /* inbox rings   */
+    __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][128]; /* 2 words/lane  */
+    __shared__ __attribute__((aligned(16))) uint16_t s_dm[WAVES][64];   /* dest masks    */
     __shared__ unsigned long long s_cnt[WAVES][K_N];
 
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t node = lane % NP, gbase = lane - node;
     if (lane < K_N) s_cnt[wv][lane] = 0;
 
-    const uint64_t n = A.d_n ? (uint64_t)*A.d_n : A.n_sys;
-    const uint64_t pool = (uint64_t)gridDim.x * WAVES * GPW;
-    const uint64_t rs = n > pool ? (n - pool + 7) / 8 : 0;
-    uint32_t shard = blockIdx.x & 7u, tried = 0;
+    const uint64_t n = Ap->d_n ? (uint64_t)*Ap->d_n : Ap->n_sys;
+    const uint32_t *list = Ap->list;
     const uint64_t G = ((uint64_t)blockIdx.x * WAVES + wv) * GPW + lane / NP;
+    uint32_t shard = blockIdx.x & 7u, tried = 0;
+    /* GEN: loop-invariant generator parameters */
+    const uint64_t gmul = GEN ? Ap->seed * 0x9E3779B97F4A7C15ULL : 0;
+    const uint64_t gfirst = GEN ? Ap->first_sys : 0;
+    const int gdist = GEN ? Ap->dist : 0;
 
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
@@ -274,18 +254,48 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
     uint64_t sys = 0;
     uint32_t rounds = 0, rmsg = 0;
     bool live = false;
-    nd.ctl = 0; nd.ip = 0; nd.nins = 0; nd.rh = 0; nd.dh = 0;
+    uint32_t tc[7] = {0, 0, 0, 0, 0, 0, 0};                                  /* TC only */
+    nd.dst = nd.caddr = nd.cval = nd.cst = nd.ctl = nd.ip = nd.nins = nd.rh = nd.nmsg = 0;
+
+    /* initializeProcessor :778-790 and main :142-146 for a new system in this lane's group */
+    auto start = [&](uint64_t s) {
+        sys = list ? (uint64_t)list[s] : s;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) nd.tc[k] = 0;
+        for (int i = 0; i < 16; ++i) s_mb[wv][i][lane] = (uint16_t)((20u * node + i) & 0xFFu);
+        nd.dst = 0xAAAAAAAAu; nd.caddr = 0xFFFFFFFFu; nd.cval = 0; nd.cst = 0xFFu;
+        nd.ctl = 0; nd.ip = 0; nd.rh = 0; nd.nmsg = 0;
+        rounds = 0;
+        if (TC) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) tc[k] = 0;
+        }
+        if (GEN) {
+            nd.nins = Ap->n_instr;
+        } else {
+            const uint32_t stride = Ap->stride;
+            const uint32_t c = Ap->counts[sys * NP + node];
+            nd.nins = c < stride ? c : stride;
+            tb = Ap->traces + (sys * NP + node) * (uint64_t)stride;
+            if (nd.nins > 0) {
+                const uint4 v = ld16(tb);
+                cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
+            }
+            if (nd.nins > 8) {
+                const uint4 v = ld16(tb + 8);
+                nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
+            }
+        }
+    };
 
     if (G < n) {
-        sys = A.list ? (uint64_t)A.list[G] : G;
         live = true;
-        start_system<NP, GEN>(nd, cur, nxt, tb, sys, node, A);
+        start(G);
     }
 
+    uint32_t wrounds = 0;    /* loop iterations of this wave (uniform) */
     for (;;) {
         if (__ballot(live) == 0) break;
+        ++wrounds;
 
         /* ---- (1) this round's action, from state at the start of the round ---------- */
         const uint32_t cnt0 = nd.rh >> 8, head0 = nd.rh & 0xFFu;
@@ -293,18 +303,18 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
         const bool canIssue = live && !hasMsg && !(nd.ctl & C_WAIT);      /* :578-581 */
         const bool doIssue = canIssue && nd.ip < nd.nins;                 /* :590-592 */
         const bool doDump = canIssue && !doIssue && !(nd.ctl & C_DUMPED); /* :688-697 */
-        nd.rh = hasMsg ? (((head0 + 1) & (RING - 1)) | ((cnt0 - 1) << 8)) : nd.rh;
-        uint32_t w = rmsg, op = rmsg & 15u;
+        const uint32_t headn = (head0 + 1 == (uint32_t)RING) ? 0u : head0 + 1;
+        nd.rh = hasMsg ? (headn | ((cnt0 - 1) << 8)) : nd.rh;
+        uint32_t w = rmsg;
         if (doIssue) {
             uint32_t ins;
             if (GEN) {
-                ins = gen_instr<NP>(A.seed, A.dist, A.first_sys + sys, node, nd.ip);
+                ins = gen_instr<NP>(gmul, gdist, gfirst + sys, node, nd.ip);
             } else {
                 const uint32_t k = nd.ip & 7u, d = sel4(cur, k >> 1);
                 ins = (k & 1u) ? (d >> 16) : (d & 0xFFFFu);
             }
-            op = (ins >> 15) ? OP_WR : OP_RD;
-            w = op | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
+            w = ((ins >> 15) ? OP_WR : OP_RD) | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
             nd.ip++;
             if (!GEN && (nd.ip & 7u) == 0 && nd.ip < nd.nins) {           /* next chunk */
 #pragma unroll
@@ -315,113 +325,101 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
                 }
             }
         }
-        op = hasMsg ? op : doIssue ? op : doDump ? OP_DUMP : OP_IDLE;
+        const uint32_t op = (hasMsg || doIssue) ? (w & 15u) : doDump ? OP_DUMP : OP_IDLE;
 
         /* ---- (2) decode + the line / directory entry / memory byte it touches -------- */
         const uint32_t a = (w >> 4) & 0x7Fu, v = (w >> 11) & 0xFFu, r2 = (w >> 19) & 7u;
-        const uint32_t excl = (w >> 22) & 1u, s = (w >> 23) & 7u;
+        const uint32_t s = (w >> 23) & 7u;
         const uint32_t H = a >> 4, blk = a & 15u, idx = a & 3u;          /* :177-184 */
         const uint32_t La = get8(nd.caddr, idx), Lv = get8(nd.cval, idx), Ls = get2(nd.cst, idx);
-        const uint32_t Db = getb16(nd.bv, blk), Ds = get2(nd.dst, blk), Mv = getb16(nd.mem, blk);
+        const uint32_t mbw = s_mb[wv][blk][lane];
+        const uint32_t Mv = mbw & 0xFFu, Db = mbw >> 8, Ds = get2(nd.dst, blk);
         const uint32_t pend = nd.ctl & 0xFFu;
-
-        const bool tRREQ = op == T_RREQ, tWREQ = op == T_WREQ, tRRD = op == T_RRD;
-        const bool tRWR = op == T_RWR, tRID = op == T_RID, tINV = op == T_INV;
-        const bool tUPG = op == T_UPG, tWBINV = op == T_WBINV, tWBINT = op == T_WBINT;
-        const bool tFLUSH = op == T_FLUSH, tFLINV = op == T_FLINV, tEVS = op == T_EVS;
-        const bool tEVM = op == T_EVM, tRD = op == OP_RD, tWR = op == OP_WR;
 
         const bool home = (H == node), atR2 = (node == r2);
         const bool hit = (La == a), valid = (Ls != CI), hitv = hit && valid;
-        const bool mOrE = (Ls <= CE);
         const uint32_t sbit = 1u << s;
         const bool sSet = (Db & sbit) != 0u;
         const uint32_t ob = Db & NPM;
         const uint32_t own = __builtin_ctz(ob | 0x80000000u);            /* findOwner :98 */
         const bool fwd = (Ds == DEM) && (own != s);      /* owner elsewhere: forward */
+        const bool isIssue = (op == OP_RD || op == OP_WR) && H < (uint32_t)NP;
 
         /* reference asserts (:189-190,:213,:299-300,:376-377,:408,:443,:489,:542-543) */
         const bool lineOK = hit || La == 0xFFu || !valid;
         const bool emNoOwner = (Ds == DEM) && ob == 0u;
-        const bool issueBad = (tRD || tWR) && H >= (uint32_t)NP;
-        const bool asrt = ((tRREQ || tWREQ || tUPG || tEVM) && !home) ||
-                          ((tRREQ || tWREQ) && emNoOwner) || (tRWR && !lineOK) ||
-                          (tFLINV && atR2 && !lineOK) || issueBad;
-        const bool rreq = tRREQ && home && !emNoOwner;
-        const bool wreq = tWREQ && home && !emNoOwner;
-        const bool upg = tUPG && home;
+        const bool asrt = ((op == T_RREQ || op == T_WREQ || op == T_UPG || op == T_EVM) && !home) ||
+                          ((op == T_RREQ || op == T_WREQ) && emNoOwner) ||
+                          (op == T_RWR && !lineOK) || (op == T_FLINV && atR2 && !lineOK) ||
+                          ((op == OP_RD || op == OP_WR) && H >= (uint32_t)NP);
+        const bool okHome = home && !emNoOwner;
 
-        /* memory: WRITE_REQUEST :379, FLUSH :276, FLUSH_INVACK :478, EVICT_MODIFIED :544 */
-        const uint32_t nMv = (home && (tWREQ || tFLUSH || tFLINV || tEVM)) ? v : Mv;
+        /* memory byte: WRITE_REQUEST :379, FLUSH :276, FLUSH_INVACK :478, EVICT_MODIFIED :544 */
+        const bool wMem = home && (op == T_WREQ || op == T_FLUSH || op == T_FLINV || op == T_EVM);
+        const uint32_t nMv = wMem ? v : Mv;
 
-        /* directory */
+        /* directory entry */
         const uint32_t evDb = Db & ~sbit;
         const uint32_t rem = __builtin_popcount(evDb & NPM);
-        const bool evsH = tEVS && home && sSet;                           /* :501-521 */
-        uint32_t nDb = Db, nDs = Ds;
-        nDb = rreq ? ((Ds == DU) ? sbit : (Db | sbit)) : nDb;            /* :196-234 */
-        nDs = rreq ? (((Ds == DU) || (Ds == DEM && !fwd)) ? DEM : DS) : nDs;
-        nDb = (wreq || upg) ? sbit : nDb;                                /* :381-433, :302-327 */
-        nDs = (wreq || upg) ? DEM : nDs;
-        nDb = (tFLINV && home) ? (1u << r2) : nDb;                       /* :479-480 */
-        nDs = (tFLINV && home) ? DEM : nDs;
-        nDb = evsH ? evDb : nDb;
-        nDs = evsH ? ((rem == 0) ? DU : (rem == 1 && Ds == DS) ? DEM : Ds) : nDs;
-        const bool evmClr = tEVM && home && Ds == DEM && sSet;            /* :545-547 */
-        nDb = evmClr ? 0u : nDb;
-        nDs = evmClr ? DU : nDs;
+        uint32_t nDb = Db, nDs = Ds, o0 = 0;
+        if (op == T_RREQ && okHome) {                                    /* :196-234 */
+            nDb = (Ds == DU) ? sbit : (Db | sbit);
+            nDs = (Ds == DS || fwd) ? DS : DEM;
+            o0 = fwd ? to(mbody(T_WBINT, a, 0, s), own)
+                     : to(mbody(T_RRD, a, Mv, 0, Ds != DS ? 1u : 0u), s);
+        }
+        if (op == T_WREQ && okHome) {                                    /* :381-433 */
+            nDb = sbit; nDs = DEM;
+            o0 = fwd ? to(mbody(T_WBINV, a, 0, s), own)
+                     : (Ds == DS) ? to(mbody(T_RID, a, Db & ~sbit & 0xFFu), s)
+                                  : to(mbody(T_RWR, a), s);
+        }
+        if (op == T_UPG && home) {                                       /* :302-327 */
+            nDb = sbit; nDs = DEM;
+            o0 = to(mbody(T_RID, a, (Ds == DS) ? (Db & ~sbit & 0xFFu) : 0u), s);
+        }
+        if (op == T_FLINV && home) { nDb = 1u << r2; nDs = DEM; }        /* :479-480 */
+        if (op == T_EVS && home && sSet) {                               /* :501-521 */
+            nDb = evDb;
+            nDs = (rem == 0) ? DU : (rem == 1 && Ds == DS) ? DEM : Ds;
+            if (rem == 1 && Ds == DS) o0 = to(mbody(T_EVS, a), __builtin_ctz((evDb & NPM) | 0x80000000u));
+        }
+        if (op == T_EVM && home && Ds == DEM && sSet) { nDb = 0; nDs = DU; } /* :545-547 */
 
-        /* sends: o0 = victim / reply / forward / flush / INV fan-out, o1 = request */
-        uint32_t o0 = 0;
-        o0 = rreq ? (fwd ? to(mbody(T_WBINT, a, 0, s), own)
-                         : to(mbody(T_RRD, a, Mv, 0, Ds != DS ? 1u : 0u), s)) : o0;
-        o0 = wreq ? (fwd ? to(mbody(T_WBINV, a, 0, s), own)
-                         : (Ds == DS) ? to(mbody(T_RID, a, Db & ~sbit & 0xFFu), s)
-                                      : to(mbody(T_RWR, a), s)) : o0;
-        o0 = upg ? to(mbody(T_RID, a, (Ds == DS) ? (Db & ~sbit & 0xFFu) : 0u), s) : o0;
-        o0 = (evsH && rem == 1 && Ds == DS)
-                 ? to(mbody(T_EVS, a), __builtin_ctz((evDb & NPM) | 0x80000000u)) : o0;
-        const bool flushOut = (tWBINT || tWBINV) && hit && mOrE;          /* :251-264, :453-466 */
-        o0 = flushOut ? (mbody(tWBINT ? T_FLUSH : T_FLINV, a, Lv, r2) | (1u << (24 + H)) |
-                         (1u << (24 + r2))) : o0;
+        /* cache side: flush forwards, INV fan-out, victim, request */
+        const bool flushOut = (op == T_WBINT || op == T_WBINV) && hit && Ls <= CE; /* :251, :453 */
+        if (flushOut)
+            o0 = mbody(op == T_WBINT ? T_FLUSH : T_FLINV, a, Lv, r2) | (1u << (24 + H)) | (1u << (24 + r2));
         const uint32_t invm = v & NPM & ~(1u << node);                   /* :350-362 */
-        o0 = (tRID && hit && invm) ? (mbody(T_INV, a) | (invm << 24)) : o0;
-        const bool isIssue = (tRD || tWR) && !issueBad;
-        const bool installRd = tRRD || (tFLUSH && atR2);                 /* :238-247, :286-295 */
-        const bool evict = (La != 0xFFu) && valid &&                      /* :742-773 */
-                           ((installRd && !hit) || (isIssue && !hitv));
-        o0 = evict ? to((Ls == CM) ? mbody(T_EVM, La, Lv) : mbody(T_EVS, La), La >> 4) : o0;
-        const bool sendReq = isIssue && (!hitv || (tWR && Ls == CS));     /* :612-629, :646-684 */
-        const uint32_t o1 = sendReq ? to(mbody(tRD ? T_RREQ : (hitv ? T_UPG : T_WREQ), a,
-                                                (tWR && !hitv) ? v : 0u), H) : 0u;
+        if (op == T_RID && hit && invm) o0 = mbody(T_INV, a) | (invm << 24);
+        const bool installRd = op == T_RRD || (op == T_FLUSH && atR2);   /* :238-247, :286-295 */
+        const bool evict = (La != 0xFFu) && valid && ((installRd && !hit) || (isIssue && !hitv));
+        if (evict)                                                       /* :742-773 */
+            o0 = to((Ls == CM) ? mbody(T_EVM, La, Lv) : mbody(T_EVS, La), La >> 4);
+        const bool sendReq = isIssue && (!hitv || (op == OP_WR && Ls == CS)); /* :612-684 */
+        const uint32_t o1 = sendReq ? to(mbody(op == OP_RD ? T_RREQ : (hitv ? T_UPG : T_WREQ), a,
+                                               (op == OP_WR && !hitv) ? v : 0u), H) : 0u;
 
         /* cache line */
-        const bool installWr = (tRWR || (tFLINV && atR2)) && lineOK;      /* :437-449, :483-495 */
+        const bool installWr = (op == T_RWR || (op == T_FLINV && atR2)) && lineOK; /* :437-495 */
         const bool issueMiss = isIssue && !hitv;
-        const bool wrHit = tWR && !issueBad && hitv;                      /* :640-659 */
-        const bool ridUp = tRID && hit && Ls != CM;                       /* :332-336 */
-        const uint32_t nLa = (installRd || installWr || issueMiss) ? a : La;
-        uint32_t nLv = Lv;
-        nLv = ridUp ? pend : nLv;
-        nLv = wrHit ? v : nLv;
-        nLv = issueMiss ? 0u : nLv;
-        nLv = installWr ? (tRWR ? pend : v) : nLv;
-        nLv = installRd ? v : nLv;
-        uint32_t nLs = Ls;
-        nLs = (tEVS && !home && s == H && hit && Ls == CS) ? CE : nLs;    /* :526-532 */
-        nLs = (tINV && hit && (Ls == CS || Ls == CE)) ? CI : nLs;         /* :366-373 */
-        nLs = flushOut ? (tWBINT ? CS : CI) : nLs;
-        nLs = ridUp ? CM : nLs;
-        nLs = wrHit ? CM : nLs;
-        nLs = issueMiss ? CI : nLs;
-        nLs = installWr ? CM : nLs;
-        nLs = installRd ? ((tRRD && excl) ? CE : CS) : nLs;
+        const bool wrHit = op == OP_WR && isIssue && hitv;                /* :640-659 */
+        const bool ridUp = op == T_RID && hit && Ls != CM;                /* :332-336 */
+        uint32_t nLa = La, nLv = Lv, nLs = Ls;
+        if (op == T_EVS && !home && s == H && hit && Ls == CS) nLs = CE;  /* :526-532 */
+        if (op == T_INV && hit && (Ls == CS || Ls == CE)) nLs = CI;       /* :366-373 */
+        if (flushOut) nLs = (op == T_WBINT) ? CS : CI;
+        if (ridUp) { nLv = pend; nLs = CM; }
+        if (wrHit) { nLv = v; nLs = CM; }
+        if (issueMiss) { nLa = a; nLv = 0; nLs = CI; }
+        if (installWr) { nLa = a; nLv = (op == T_RWR) ? pend : v; nLs = CM; }
+        if (installRd) { nLa = a; nLv = v; nLs = (op == T_RRD && ((w >> 22) & 1u)) ? CE : CS; }
 
         /* waitingForReply / pendingWriteValue / assert flag */
-        const bool clrWait = installRd || installWr || tRID;
         uint32_t ctl = nd.ctl;
-        ctl = sendReq ? (ctl | C_WAIT) : clrWait ? (ctl & ~C_WAIT) : ctl;
-        ctl = (tWR && !issueBad) ? ((ctl & ~0xFFu) | v) : ctl;           /* :633 */
+        ctl = (installRd || installWr || op == T_RID) ? (ctl & ~C_WAIT) : ctl;
+        ctl = sendReq ? (ctl | C_WAIT) : ctl;
+        ctl = (op == OP_WR && isIssue) ? ((ctl & ~0xFFu) | v) : ctl;     /* :633 */
         ctl = asrt ? (ctl | C_ASSERT) : ctl;
         nd.ctl = ctl;
 
@@ -430,52 +428,50 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
         nd.cval = set8(nd.cval, idx, nLv);
         nd.cst = set2(nd.cst, idx, nLs);
         nd.dst = set2(nd.dst, blk, nDs);
-        setb16(nd.bv, blk, nDb);
-        setb16(nd.mem, blk, nMv);
-        {
-            const uint32_t inc = (op <= T_EVM) ? (1u << ((op & 1u) * 16)) : 0u, q = op >> 1;
+        s_mb[wv][blk][lane] = (uint16_t)(nMv | (nDb << 8));
+        const bool isMsg = op <= T_EVM;
+        nd.nmsg += isMsg ? 1u : 0u;
+        if (TC) {
+            const uint32_t inc = isMsg ? (1u << ((op & 1u) * 16)) : 0u, q = op >> 1;
 #pragma unroll
-            for (uint32_t k = 0; k < 7; ++k) nd.tc[k] += (q == k) ? inc : 0u;
+            for (uint32_t k = 0; k < 7; ++k) tc[k] += (q == k) ? inc : 0u;
         }
         if (doDump) {                                                    /* :688-697 */
-            nd.ctl |= C_DUMPED;
-            nd.dh = node_hash<15>(node, nd, 2u);
-            if (A.snap) store_rec(&A.snap_dump[sys * NP + node], nd, 2u);
+            nd.ctl |= C_DUMPED;               /* printProcessorState(threadId, node), :695 */
+            store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8, nd, s_mb, wv, lane, 2u);
         }
 
         /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         reinterpret_cast<uint2 *>(s_out[wv])[lane] = make_uint2(o0, o1);
+        s_dm[wv][lane] = (uint16_t)((o0 >> 24) | ((o1 >> 24) << 8));
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t R = 0;                  /* bit 2*sender+word: that word is addressed to me */
-        {
-            const uint4 *g = reinterpret_cast<const uint4 *>(&s_out[wv][2 * gbase]);
-#pragma unroll
-            for (int q = 0; q < NP / 2; ++q) {
-                const uint4 x = g[q];
-                R |= (__builtin_amdgcn_ubfe(x.x, 24 + node, 1) << (4 * q)) |
-                     (__builtin_amdgcn_ubfe(x.y, 24 + node, 1) << (4 * q + 1)) |
-                     (__builtin_amdgcn_ubfe(x.z, 24 + node, 1) << (4 * q + 2)) |
-                     (__builtin_amdgcn_ubfe(x.w, 24 + node, 1) << (4 * q + 3));
-            }
+        uint32_t R;                      /* bit 2*sender+word: that word is addressed to me */
+        if (NP == 8) {
+            const uint4 x = *reinterpret_cast<const uint4 *>(&s_dm[wv][gbase]);
+            R = gather4(x.x, node) | (gather4(x.y, node) << 4) | (gather4(x.z, node) << 8) |
+                (gather4(x.w, node) << 12);
+        } else {
+            const uint2 x = *reinterpret_cast<const uint2 *>(&s_dm[wv][gbase]);
+            R = gather4(x.x, node) | (gather4(x.y, node) << 4);
         }
         {
             const uint32_t hh = nd.rh & 0xFFu;
             uint32_t cc = nd.rh >> 8;
-            bool ovf = false;
             while (R) {
                 const uint32_t j = __builtin_ctz(R);
                 R &= R - 1;
                 const uint32_t x = s_out[wv][2 * gbase + j];
                 if (cc < (uint32_t)RING) {
-                    s_ring[wv][(hh + cc) & (RING - 1)][lane] = (x & 0x7FFFFFu) | ((j >> 1) << 23);
+                    const uint32_t slot = hh + cc;
+                    s_ring[wv][slot >= (uint32_t)RING ? slot - RING : slot][lane] =
+                        (x & 0x7FFFFFu) | ((j >> 1) << 23);
                     ++cc;
                 } else {
-                    ovf = true;
+                    nd.ctl |= C_OVF;
                 }
             }
             nd.rh = hh | (cc << 8);
-            if (ovf) nd.ctl |= C_OVF;
             rmsg = s_ring[wv][hh][lane];          /* next round's head, prefetched */
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -500,45 +496,34 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
                 else if (gbad) st = DSM_RING_OVERFLOW;
                 else if (gact == 0) st = (dmask == NPM) ? DSM_COMPLETED : DSM_DEADLOCKED;
                 else st = DSM_ROUND_LIMIT;
-                const bool handoff = (st == DSM_RING_OVERFLOW) && A.ovf_list;
+                const bool handoff = !FB && (st == DSM_RING_OVERFLOW);
                 const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
-                uint64_t fh = node_hash<16>(node, nd, fl);
-                if (A.snap && !handoff) store_rec(&A.snap_final[sys * NP + node], nd, fl);
-                fh = gsum64<NP>(fh);
-                const uint64_t dh = gsum64<NP>(nd.dh);
-                const uint32_t ins = gsum32<NP>(nd.ip);
-                uint32_t msgs = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < 7; ++k) msgs += (nd.tc[k] & 0xFFFFu) + (nd.tc[k] >> 16);
-                msgs = gsum32<NP>(msgs);
+                if (!handoff) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, wv, lane, fl);
+                const uint32_t ins = gsum32<NP>(nd.ip), msgs = gsum32<NP>(nd.nmsg);
                 uint32_t nlo = 0xFFFFFFFFu, nhi = 0xFFFFFFFFu;
                 if (node == 0) {
                     if (handoff) {
-                        const uint32_t pos = atomicAdd(A.ovf_count, 1u);
-                        A.ovf_list[pos] = (uint32_t)sys;
+                        const uint32_t pos = atomicAdd(Ap->ovf_count, 1u);
+                        Ap->ovf_list[pos] = (uint32_t)sys;
                         atomicAdd(&s_cnt[wv][K_OVFRERUN], 1ull);
                     } else {
-                        if (A.results) {
-                            uint4 *rp = reinterpret_cast<uint4 *>(&A.results[sys]);
-                            rp[0] = make_uint4(st | (dmask << 8), rounds, msgs, ins);
-                            rp[1] = make_uint4((uint32_t)dh, (uint32_t)(dh >> 32), (uint32_t)fh,
-                                               (uint32_t)(fh >> 32));
-                        }
+                        reinterpret_cast<uint4 *>(Ap->results)[2 * sys] =
+                            make_uint4(st | (dmask << 8), rounds, msgs, ins);
                         atomicAdd(&s_cnt[wv][K_MSGS], (unsigned long long)msgs);
                         atomicAdd(&s_cnt[wv][K_INSTRS], (unsigned long long)ins);
                         atomicAdd(&s_cnt[wv][K_ROUNDS], (unsigned long long)rounds);
                         atomicAdd(&s_cnt[wv][K_SYSTEMS], 1ull);
                         atomicAdd(&s_cnt[wv][K_STATUS + st], 1ull);
-                        atomicAdd(&s_cnt[wv][K_DHASH], (unsigned long long)dh);
-                        atomicAdd(&s_cnt[wv][K_FHASH], (unsigned long long)fh);
                         atomicMax(&s_cnt[wv][K_MAXR], (unsigned long long)rounds);
                     }
                     /* next system: static first assignment, then 8 sharded counters */
+                    const uint64_t pool = (uint64_t)gridDim.x * WAVES * GPW;
+                    const uint64_t rs = n > pool ? (n - pool + 7) / 8 : 0;
                     while (tried < 8) {
                         const uint64_t lo = pool + (uint64_t)shard * rs;
                         const uint64_t len = (n > lo) ? ((n - lo) < rs ? (n - lo) : rs) : 0;
                         if (len) {
-                            const uint32_t r = atomicAdd(&A.claim[shard * 32u], 1u);
+                            const uint32_t r = atomicAdd(&Ap->claim[shard * 32u], 1u);
                             if (r < len) {
                                 const uint64_t nl = lo + r;
                                 nlo = (uint32_t)nl; nhi = (uint32_t)(nl >> 32);
@@ -549,31 +534,27 @@ __global__ void __launch_bounds__(64 * WAVES) sim_kernel(SimArgs A) {
                         ++tried;
                     }
                 }
-                if (!handoff) {
+                if (TC && !handoff) {
 #pragma unroll
                     for (uint32_t t = 0; t < DSM_NTYPES; ++t) {
-                        const uint32_t c = (nd.tc[t >> 1] >> ((t & 1u) * 16)) & 0xFFFFu;
+                        const uint32_t c = (tc[t >> 1] >> ((t & 1u) * 16)) & 0xFFFFu;
                         if (c) atomicAdd(&s_cnt[wv][t], (unsigned long long)c);
                     }
                 }
                 nlo = __shfl(nlo, (int)gbase, 64);
                 nhi = __shfl(nhi, (int)gbase, 64);
                 const uint64_t nl = ((uint64_t)nhi << 32) | nlo;
-                rounds = 0;
-                if (nl != NO_SYS) {
-                    sys = A.list ? (uint64_t)A.list[nl] : nl;
-                    start_system<NP, GEN>(nd, cur, nxt, tb, sys, node, A);
-                } else {
-                    live = false;
-                }
+                if (nl != NO_SYS) start(nl);
+                else live = false;
             }
         }
     }
 
     /* publish this wave's counters */
+    if (lane == 0) s_cnt[wv][K_WROUNDS] = wrounds;
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if (lane < K_N)
-        A.partials[((uint64_t)blockIdx.x * WAVES + wv) * K_N + lane] = s_cnt[wv][lane];
+        Ap->partials[((uint64_t)blockIdx.x * WAVES + wv) * K_N + lane] = s_cnt[wv][lane];
 }
 
 /* ---- partial-counter reduction (deterministic, one block) ---------------------------- */
@@ -594,10 +575,68 @@ __global__ void __launch_bounds__(256) reduce_kernel(const unsigned long long *p
     }
 }
 
+/* ---- digest: per-system hashes of the node records ------------------------------------
+ * One lane per node record pair; dump_hash sums the 15-word hash of every dumped node's
+ * dump record, final_hash the 16-word hash of every final record.  Memory-
+ * bound (128 B read per node); keeps the 64-bit hashing out of the transition kernel. */
+template <int NP>
+__global__ void __launch_bounds__(256) digest_kernel(uint64_t n_sys, const uint4 *recs,
+                                                     dsm_sys_result *results,
+                                                     unsigned long long *partials) {
+    __shared__ unsigned long long s_sum[2][4];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, node = lane % NP;
+    uint64_t adh = 0, afh = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i - node < n_sys * NP;
+         i += (uint64_t)gridDim.x * 256) {
+        const uint64_t sys = i / NP;
+        const bool ok = sys < n_sys;
+        uint64_t dh = 0, fh = 0;
+        if (ok) {
+            const uint4 *r = recs + i * 8;
+            const uint32_t dmask = results[sys].status >> 8;
+            uint64_t hd = 0x9E3779B97F4A7C15ULL * (uint64_t)(node + 1), hf = hd;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 d = r[q], f = r[4 + q];
+                const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, fw[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int wi = 4 * q + k;
+                    if (wi < 15) hd = fmix64(hd ^ ((uint64_t)dw[k] | ((uint64_t)wi << 32)));
+                    hf = fmix64(hf ^ ((uint64_t)fw[k] | ((uint64_t)wi << 32)));
+                }
+            }
+            dh = ((dmask >> node) & 1u) ? hd : 0;
+            fh = hf;
+        }
+        dh = gsum64<NP>(dh);
+        fh = gsum64<NP>(fh);
+        if (ok && node == 0) {
+            results[sys].dump_hash = dh;
+            results[sys].final_hash = fh;
+            adh += dh;
+            afh += fh;
+        }
+    }
+    /* block partial: wave sums, then one write per block */
+    for (int o = 1; o < 64; o <<= 1) {
+        adh += ((uint64_t)__shfl_xor((uint32_t)(adh >> 32), o, 64) << 32) | __shfl_xor((uint32_t)adh, o, 64);
+        afh += ((uint64_t)__shfl_xor((uint32_t)(afh >> 32), o, 64) << 32) | __shfl_xor((uint32_t)afh, o, 64);
+    }
+    if (lane == 0) { s_sum[0][wv] = adh; s_sum[1][wv] = afh; }
+    __syncthreads();
+    if (threadIdx.x < K_N) {
+        unsigned long long v = 0;
+        if (threadIdx.x == K_DHASH) v = s_sum[0][0] + s_sum[0][1] + s_sum[0][2] + s_sum[0][3];
+        if (threadIdx.x == K_FHASH) v = s_sum[1][0] + s_sum[1][1] + s_sum[1][2] + s_sum[1][3];
+        partials[(uint64_t)blockIdx.x * K_N + threadIdx.x] = v;
+    }
+}
+
 /* ---- trace generator ------------------------------------------------------------------
  * One workgroup iteration = one (system, node) slot of `stride` instructions; each lane
- * produces 16-byte chunks (8 instructions) and streams them out with non-temporal stores
- * (written once, read later by a different kernel).  No 64-bit divisions in the index math. */
+ * produces 16-byte chunks (8 instructions, two splitmix64 calls) and streams them out with
+ * non-temporal stores (written once, read later by another kernel). */
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <int NP>
@@ -637,24 +676,47 @@ __global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist, uint6
 }
 
 /* ---- kernel table ------------------------------------------------------------------- */
-typedef void (*sim_fn)(SimArgs);
+typedef void (*sim_fn)(const SimArgs *);
 
-template <int NP, bool GEN>
+/* Occupancy target of the transition kernel (amdgpu_waves_per_eu): the register budget is
+ * the lever between latency hiding and spilling; DSM_OCC selects a variant for A/B runs. */
+static int occ_choice() {
+    const char *e = getenv("DSM_OCC");
+    const int v = e ? atoi(e) : 5;
+    return (v == 1 || v == 4 || v == 6) ? v : 5;
+}
+template <int NP, bool GEN, bool TC>
 sim_fn fast_kernel(int ring) {
     switch (ring) {
-    case 4: return sim_kernel<NP, 4, 4, GEN>;
-    case 8: return sim_kernel<NP, 8, 4, GEN>;
-    case 32: return sim_kernel<NP, 32, 4, GEN>;
-    default: return sim_kernel<NP, 16, 4, GEN>;
+    case 4: return sim_kernel<NP, 4, 4, GEN, TC>;
+    case 8: return sim_kernel<NP, 8, 4, GEN, TC>;
+    case 16: return sim_kernel<NP, 16, 4, GEN, TC>;
+    default:
+        if (NP == 8 && !TC) {
+            switch (occ_choice()) {
+            case 1: return sim_kernel<NP, 12, 4, GEN, TC, 1>;
+            case 4: return sim_kernel<NP, 12, 4, GEN, TC, 4>;
+            case 6: return sim_kernel<NP, 12, 4, GEN, TC, 6>;
+            default: break;
+            }
+        }
+        return sim_kernel<NP, 12, 4, GEN, TC>;
     }
 }
-sim_fn pick_fast(int np, int ring, bool gen) {
-    if (np == 4) return gen ? fast_kernel<4, true>(ring) : fast_kernel<4, false>(ring);
-    return gen ? fast_kernel<8, true>(ring) : fast_kernel<8, false>(ring);
+template <int NP, bool GEN>
+sim_fn fast_np_gen(int ring, bool tc) { return tc ? fast_kernel<NP, GEN, true>(ring) : fast_kernel<NP, GEN, false>(ring); }
+sim_fn pick_fast(int np, int ring, bool gen, bool tc) {
+    if (np == 4) return gen ? fast_np_gen<4, true>(ring, tc) : fast_np_gen<4, false>(ring, tc);
+    return gen ? fast_np_gen<8, true>(ring, tc) : fast_np_gen<8, false>(ring, tc);
 }
-sim_fn pick_fallback(int np, bool gen) {
-    if (np == 4) return gen ? sim_kernel<4, 256, 1, true> : sim_kernel<4, 256, 1, false>;
-    return gen ? sim_kernel<8, 256, 1, true> : sim_kernel<8, 256, 1, false>;
+template <int NP, bool GEN>
+sim_fn fb_np_gen(bool tc) { return tc ? sim_kernel<NP, FB_RING, 1, GEN, true, 1> : sim_kernel<NP, FB_RING, 1, GEN, false, 1>; }
+sim_fn pick_fallback(int np, bool gen, bool tc) {
+    if (np == 4) return gen ? fb_np_gen<4, true>(tc) : fb_np_gen<4, false>(tc);
+    return gen ? fb_np_gen<8, true>(tc) : fb_np_gen<8, false>(tc);
+}
+int lds_bytes(int ring, int waves) {
+    return waves * (16 * 64 * 2 + ring * 64 * 4 + 128 * 4 + 64 * 2 + K_N * 8);
 }
 
 }  // namespace
@@ -670,6 +732,7 @@ struct dsm_ctx {
     hipStream_t stream;
     int cus;
     unsigned int *d_ctrl;            /* claim shards (fast, fallback) + overflow count      */
+    SimArgs *d_args;                 /* [0] fast kernel, [1] 256-deep re-run                */
     unsigned long long *d_partials;
     size_t partials_waves;
     uint32_t *d_ovf_list;
@@ -681,10 +744,11 @@ struct dsm_ctx {
     dsm_sys_result *d_res;
     size_t res_cap;
     dsm_counters *d_cnt;
-    dsm_node_state *d_snap_dump, *d_snap_final;
-    size_t snap_cap_d, snap_cap_f;
-    uint64_t snap_n;
-    hipEvent_t ev0, ev1;
+    uint4 *d_recs;                   /* [sys][node][dump, final] node records of the last run */
+    size_t recs_cap;
+    uint64_t recs_n;
+    SimArgs *h_args;                 /* pinned host staging for the argument blocks         */
+    hipEvent_t ev0, ev1, ev_args;
     int timed;
     dsm_launch_info info;
 };
@@ -718,8 +782,8 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     *out = nullptr;
     if (cfg->np != 4 && cfg->np != 8) return DSM_E_INVAL;
     if (cfg->max_instr == 0 || cfg->max_instr > DSM_MAX_INSTR || (cfg->max_instr & 7u)) return DSM_E_INVAL;
-    int ring = cfg->ring_cap ? (int)cfg->ring_cap : 16;
-    if (ring != 4 && ring != 8 && ring != 16 && ring != 32) return DSM_E_INVAL;
+    int ring = cfg->ring_cap ? (int)cfg->ring_cap : 12;
+    if (ring != 4 && ring != 8 && ring != 12 && ring != 16) return DSM_E_INVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return DSM_E_DEVICE;
     hipDeviceProp_t prop;
@@ -734,6 +798,9 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void **)&c->d_ctrl, CTRL_WORDS * sizeof(unsigned int)) != hipSuccess ||
+        hipMalloc((void **)&c->d_args, 2 * sizeof(SimArgs)) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_args, 2 * sizeof(SimArgs), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_args, hipEventDisableTiming) != hipSuccess ||
         hipMalloc((void **)&c->d_cnt, sizeof(dsm_counters)) != hipSuccess) {
         dsm_close(c);
         return DSM_E_DEVICE;
@@ -751,11 +818,13 @@ extern "C" void dsm_close(dsm_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *ptrs[] = {c->d_ctrl, c->d_partials, c->d_ovf_list, c->d_traces, c->d_counts,
-                    c->d_res, c->d_cnt, c->d_snap_dump, c->d_snap_final};
+    void *ptrs[] = {c->d_ctrl, c->d_args, c->d_partials, c->d_ovf_list, c->d_traces, c->d_counts,
+                    c->d_res, c->d_cnt, c->d_recs};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    if (c->h_args) (void)hipHostFree(c->h_args);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev_args) (void)hipEventDestroy(c->ev_args);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     free(c);
 }
@@ -774,7 +843,8 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     if (n_sys > 0xFFFFFFFFull) return DSM_E_INVAL;
     HIPCK(hipSetDevice(c->device));
     const int np = c->cfg.np, gpw = 64 / np;
-    sim_fn fast = pick_fast(np, c->ring, gen), fb = pick_fallback(np, gen);
+    const bool tc = (c->cfg.flags & DSM_F_TYPE_COUNTS) != 0;
+    sim_fn fast = pick_fast(np, c->ring, gen, tc), fb = pick_fallback(np, gen, tc);
     int nb_fast = 0, nb_fb = 0;
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fast, (const void *)fast, 256, 0));
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fb, (const void *)fb, 64, 0));
@@ -783,20 +853,25 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     int grid_fast = (int)((uint64_t)nb_fast * c->cus < want ? (uint64_t)nb_fast * c->cus : want);
     int grid_fb = nb_fb * c->cus;
     if (grid_fb > 1024) grid_fb = 1024;
-    const size_t waves = (size_t)grid_fast * 4 + (size_t)grid_fb;
+    uint64_t dblocks = (n_sys * np + 255) / 256;
+    if (dblocks > (uint64_t)c->cus * 8) dblocks = (uint64_t)c->cus * 8;
+    const size_t waves = (size_t)grid_fast * 4 + (size_t)grid_fb + (size_t)dblocks;
     int rc;
     if ((rc = ensure(&c->d_partials, &c->partials_waves, waves * K_N))) return rc;
     if ((rc = ensure(&c->d_ovf_list, &c->ovf_cap, (size_t)n_sys))) return rc;
-    if (c->cfg.flags & DSM_F_SNAPSHOTS) {
-        if ((rc = ensure(&c->d_snap_dump, &c->snap_cap_d, (size_t)n_sys * np))) return rc;
-        if ((rc = ensure(&c->d_snap_final, &c->snap_cap_f, (size_t)n_sys * np))) return rc;
-        HIPCK(hipMemsetAsync(c->d_snap_dump, 0, (size_t)n_sys * np * sizeof(dsm_node_state), st));
-        HIPCK(hipMemsetAsync(c->d_snap_final, 0, (size_t)n_sys * np * sizeof(dsm_node_state), st));
-        c->snap_n = n_sys;
+    if ((rc = ensure(&c->d_recs, &c->recs_cap, (size_t)n_sys * np * 8))) return rc;
+    if (!d_results) {   /* the engine needs the per-system header even if the caller does not */
+        if ((rc = ensure(&c->d_res, &c->res_cap, (size_t)n_sys + 1))) return rc;
+        d_results = c->d_res;
     }
+    if (c->cfg.flags & DSM_F_SNAPSHOTS)   /* nodes that never dump read back as zeros */
+        HIPCK(hipMemsetAsync(c->d_recs, 0, (size_t)n_sys * np * 128, st));
+    c->recs_n = n_sys;
     HIPCK(hipMemsetAsync(c->d_ctrl, 0, CTRL_WORDS * sizeof(unsigned int), st));
 
-    SimArgs A;
+    /* the pinned staging block may still be read by the previous run's copy */
+    HIPCK(hipEventSynchronize(c->ev_args));
+    SimArgs &A = c->h_args[0];
     memset(&A, 0, sizeof A);
     A.traces = d_traces;
     A.counts = d_counts;
@@ -806,27 +881,38 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.first_sys = first_sys;
     A.seed = gen ? g->seed : 0;
     A.dist = gen ? g->dist : 0;
-    A.snap = (c->cfg.flags & DSM_F_SNAPSHOTS) ? 1 : 0;
     A.results = d_results;
-    A.snap_dump = c->d_snap_dump;
-    A.snap_final = c->d_snap_final;
+    A.recs = c->d_recs;
     A.partials = c->d_partials;
     A.claim = c->d_ctrl + CTRL_FAST;
     A.ovf_list = c->d_ovf_list;
     A.ovf_count = c->d_ctrl + CTRL_OVF;
-    if (c->ev0) HIPCK(hipEventRecord(c->ev0, st));
-    hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(256), 0, st, A);
-    HIPCK(hipGetLastError());
-    if (c->ev1) { HIPCK(hipEventRecord(c->ev1, st)); c->timed = 1; }
-
-    SimArgs B = A;
+    SimArgs &B = c->h_args[1];
+    B = A;
     B.d_n = c->d_ctrl + CTRL_OVF;
     B.list = c->d_ovf_list;
     B.partials = c->d_partials + (size_t)grid_fast * 4 * K_N;
     B.claim = c->d_ctrl + CTRL_FB;
     B.ovf_list = nullptr;
     B.ovf_count = nullptr;
-    hipLaunchKernelGGL(fb, dim3(grid_fb), dim3(64), 0, st, B);
+    HIPCK(hipMemcpyAsync(c->d_args, c->h_args, 2 * sizeof(SimArgs), hipMemcpyHostToDevice, st));
+    HIPCK(hipEventRecord(c->ev_args, st));
+
+    if (c->ev0) HIPCK(hipEventRecord(c->ev0, st));
+    hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(256), 0, st, (const SimArgs *)c->d_args);
+    HIPCK(hipGetLastError());
+    if (c->ev1) { HIPCK(hipEventRecord(c->ev1, st)); c->timed = 1; }
+
+    hipLaunchKernelGGL(fb, dim3(grid_fb), dim3(64), 0, st, (const SimArgs *)(c->d_args + 1));
+    HIPCK(hipGetLastError());
+
+    unsigned long long *dpart = c->d_partials + ((size_t)grid_fast * 4 + grid_fb) * K_N;
+    if (np == 4)
+        hipLaunchKernelGGL(digest_kernel<4>, dim3((unsigned)dblocks), dim3(256), 0, st, n_sys,
+                           (const uint4 *)c->d_recs, d_results, dpart);
+    else
+        hipLaunchKernelGGL(digest_kernel<8>, dim3((unsigned)dblocks), dim3(256), 0, st, n_sys,
+                           (const uint4 *)c->d_recs, d_results, dpart);
     HIPCK(hipGetLastError());
 
     hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, st, c->d_partials, (int)waves,
@@ -838,7 +924,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     c->info.waves_per_cu = nb_fast * 4;
     c->info.cus = c->cus;
     c->info.ring_cap = c->ring;
-    c->info.lds_bytes_per_block = 4 * (c->ring * 64 * 4 + 64 * 8 + K_N * 8);
+    c->info.lds_bytes_per_block = lds_bytes(c->ring, 4);
     return DSM_OK;
 }
 
@@ -942,13 +1028,13 @@ extern "C" int dsm_last_kernel_ms(dsm_ctx *c, float *ms) {
 extern "C" int dsm_get_node_state(dsm_ctx *c, uint64_t sys, int node, dsm_node_state *dump,
                                   dsm_node_state *final_state) {
     if (!c || node < 0 || node >= c->cfg.np) return DSM_E_INVAL;
-    if (!(c->cfg.flags & DSM_F_SNAPSHOTS) || !c->d_snap_dump) return DSM_E_STATE;
-    if (sys >= c->snap_n) return DSM_E_INVAL;
+    if (!(c->cfg.flags & DSM_F_SNAPSHOTS) || !c->d_recs) return DSM_E_STATE;
+    if (sys >= c->recs_n) return DSM_E_INVAL;
     HIPCK(hipSetDevice(c->device));
     HIPCK(hipStreamSynchronize(c->stream));
     HIPCK(hipDeviceSynchronize());
-    const size_t i = (size_t)sys * c->cfg.np + node;
-    if (dump) HIPCK(hipMemcpy(dump, c->d_snap_dump + i, sizeof *dump, hipMemcpyDeviceToHost));
-    if (final_state) HIPCK(hipMemcpy(final_state, c->d_snap_final + i, sizeof *final_state, hipMemcpyDeviceToHost));
+    const size_t i = ((size_t)sys * c->cfg.np + node) * 8;
+    if (dump) HIPCK(hipMemcpy(dump, c->d_recs + i, sizeof *dump, hipMemcpyDeviceToHost));
+    if (final_state) HIPCK(hipMemcpy(final_state, c->d_recs + i + 4, sizeof *final_state, hipMemcpyDeviceToHost));
     return DSM_OK;
 }

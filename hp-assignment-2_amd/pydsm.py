@@ -21,14 +21,15 @@ STATUS_NAMES = ["COMPLETED", "DEADLOCKED", "RING_OVERFLOW", "ASSERT_FAILED", "RO
 DIST = {"uniform": 0, "hot": 1, "evict": 2}
 F_SNAPSHOTS = 1
 F_TIMING = 2
+F_TYPE_COUNTS = 4
 
 RESULT_DTYPE = np.dtype([("status", "<u4"), ("rounds", "<u4"), ("msgs", "<u4"),
                          ("instrs", "<u4"), ("dump_hash", "<u8"), ("final_hash", "<u8")])
 COUNTER_FIELDS = ([f"msgs_{t}" for t in TYPE_NAMES] +
                   ["msgs", "instrs", "rounds", "systems"] +
                   [f"status_{s}" for s in STATUS_NAMES] +
-                  ["sum_dump_hash", "sum_final_hash", "max_rounds", "overflow_reruns"] +
-                  [f"reserved{i}" for i in range(6)])
+                  ["sum_dump_hash", "sum_final_hash", "max_rounds", "overflow_reruns",
+                   "wave_rounds"] + [f"reserved{i}" for i in range(5)])
 assert len(COUNTER_FIELDS) == 32
 
 E_INVAL, E_DEVICE, E_NOMEM, E_IO, E_FORMAT, E_STATE, E_RANGE = -1, -2, -3, -4, -5, -6, -7
@@ -130,11 +131,13 @@ def device_count():
 class Engine:
     """One dsm_ctx: np nodes per system, trace stride max_instr, bound to `device`."""
 
-    def __init__(self, np_=8, max_instr=4096, ring_cap=0, snapshots=False, device=0, timing=False):
+    def __init__(self, np_=8, max_instr=4096, ring_cap=0, snapshots=False, device=0, timing=False,
+                 type_counts=False):
         self.np = np_
         self.max_instr = max_instr
         self.cfg = Config(np_, max_instr, ring_cap,
-                          (F_SNAPSHOTS if snapshots else 0) | (F_TIMING if timing else 0))
+                          (F_SNAPSHOTS if snapshots else 0) | (F_TIMING if timing else 0) |
+                          (F_TYPE_COUNTS if type_counts else 0))
         self.ctx = ctypes.c_void_p()
         _check(lib().dsm_open(device, ctypes.byref(self.cfg), ctypes.byref(self.ctx)), "dsm_open")
 

