@@ -11,9 +11,10 @@
  * Mapping (one wave64 = 64/NP systems, one lane = one node):
  *   - per-node registers: directory states (2 bits x 16), cache addresses / values (one byte
  *     per line), cache states (2 bits x 4), control word, counters;
- *   - per-node LDS column s_mb[wave][block][lane] = memory byte | bitVector byte << 8, so a
- *     message touches its home block with one ds_read_u16 / ds_write_b16 (bank = lane / 2,
- *     conflict-free) instead of a runtime byte select over 8 registers;
+ *   - per-node LDS column s_mb[wave][block/2][lane] (one dword per lane holds two blocks'
+ *     memory byte | bitVector byte << 8), so a message touches its home block with one
+ *     ds_read_u16 / ds_write_b16 (bank = lane % 32: conflict-free) instead of a runtime
+ *     byte select over 8 registers;
  *   - inboxes: LDS rings s_ring[wave][slot][lane] (bank = lane % 32, conflict-free);
  *   - a round: every lane takes one action (predicated data flow, no per-type branches),
  *     writes <= 2 outgoing words + their destination masks to LDS; each receiver gathers
@@ -166,20 +167,19 @@ DEVI uint32_t rec_word(const Node &nd, const uint32_t (&mb)[8], uint32_t flags, 
 }
 /* memory (words 0-3) and bitVector (words 4-7) bytes of this lane's node, from LDS */
 template <int WAVES>
-DEVI void load_mb(const uint16_t (&smb)[WAVES][16][64], uint32_t wv, uint32_t lane,
+DEVI void load_mb(const uint32_t (&smb)[WAVES][8][64], uint32_t wv, uint32_t lane,
                   uint32_t (&mb)[8]) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) mb[k] = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t x = smb[wv][i][lane];
-        mb[i >> 2] |= (x & 0xFFu) << (8 * (i & 3));
-        mb[4 + (i >> 2)] |= (x >> 8) << (8 * (i & 3));
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = smb[wv][2 * k][lane], y = smb[wv][2 * k + 1][lane];
+        /* x = b0 | v0 << 8 | b1 << 16 | v1 << 24, y likewise for blocks 4k+2, 4k+3 */
+        mb[k] = __builtin_amdgcn_perm(y, x, 0x06040200u);      /* bytes b0 b1 b2 b3 */
+        mb[4 + k] = __builtin_amdgcn_perm(y, x, 0x07050301u);  /* bytes v0 v1 v2 v3 */
     }
 }
 /* store this lane's 64-byte node record (dsm_node_state) */
 template <int WAVES>
-DEVI void store_rec(uint4 *dst, const Node &nd, const uint16_t (&smb)[WAVES][16][64],
+DEVI void store_rec(uint4 *dst, const Node &nd, const uint32_t (&smb)[WAVES][8][64],
                     uint32_t wv, uint32_t lane, uint32_t flags) {
     uint32_t mb[8];
     load_mb<WAVES>(smb, wv, lane, mb);
@@ -229,7 +229,7 @@ sim_kernel(const SimArgs *Ap) {
     /* TC: per-type message counters (DSM_F_TYPE_COUNTS), 16-bit fields per node and
      * system, added to the wave counters when the system finishes (exact per system). */
 
-    __shared__ uint16_t s_mb[WAVES][16][64];                           /* mem | bv << 8 */
+    __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
     __shared__ uint32_t s_ring[WAVES][RING][64];                       /* inbox rings   */
     __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][128]; /* 2 words/lane  */
     __shared__ __attribute__((aligned(16))) uint16_t s_dm[WAVES][64];   /* dest masks    */
@@ -261,7 +261,8 @@ sim_kernel(const SimArgs *Ap) {
     auto start = [&](uint64_t s) {
         sys = list ? (uint64_t)list[s] : s;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s_mb[wv][i][lane] = (uint16_t)((20u * node + i) & 0xFFu);
+        for (int i = 0; i < 8; ++i)
+            s_mb[wv][i][lane] = ((20u * node + 2 * i) & 0xFFu) | (((20u * node + 2 * i + 1) & 0xFFu) << 16);
         nd.dst = 0xAAAAAAAAu; nd.caddr = 0xFFFFFFFFu; nd.cval = 0; nd.cst = 0xFFu;
         nd.ctl = 0; nd.ip = 0; nd.rh = 0; nd.nmsg = 0;
         rounds = 0;
@@ -332,7 +333,8 @@ sim_kernel(const SimArgs *Ap) {
         const uint32_t s = (w >> 23) & 7u;
         const uint32_t H = a >> 4, blk = a & 15u, idx = a & 3u;          /* :177-184 */
         const uint32_t La = get8(nd.caddr, idx), Lv = get8(nd.cval, idx), Ls = get2(nd.cst, idx);
-        const uint32_t mbw = s_mb[wv][blk][lane];
+        uint16_t *const mbp = reinterpret_cast<uint16_t *>(&s_mb[wv][blk >> 1][lane]) + (blk & 1u);
+        const uint32_t mbw = *mbp;
         const uint32_t Mv = mbw & 0xFFu, Db = mbw >> 8, Ds = get2(nd.dst, blk);
         const uint32_t pend = nd.ctl & 0xFFu;
 
@@ -428,7 +430,7 @@ sim_kernel(const SimArgs *Ap) {
         nd.cval = set8(nd.cval, idx, nLv);
         nd.cst = set2(nd.cst, idx, nLs);
         nd.dst = set2(nd.dst, blk, nDs);
-        s_mb[wv][blk][lane] = (uint16_t)(nMv | (nDb << 8));
+        *mbp = (uint16_t)(nMv | (nDb << 8));
         const bool isMsg = op <= T_EVM;
         nd.nmsg += isMsg ? 1u : 0u;
         if (TC) {
@@ -682,8 +684,8 @@ typedef void (*sim_fn)(const SimArgs *);
  * the lever between latency hiding and spilling; DSM_OCC selects a variant for A/B runs. */
 static int occ_choice() {
     const char *e = getenv("DSM_OCC");
-    const int v = e ? atoi(e) : 5;
-    return (v == 1 || v == 4 || v == 6) ? v : 5;
+    const int v = e ? atoi(e) : 6;     /* measured best on MI355X (tools/ab_occ.py) */
+    return (v == 1 || v == 4 || v == 5) ? v : 6;
 }
 template <int NP, bool GEN, bool TC>
 sim_fn fast_kernel(int ring) {
@@ -696,8 +698,8 @@ sim_fn fast_kernel(int ring) {
             switch (occ_choice()) {
             case 1: return sim_kernel<NP, 12, 4, GEN, TC, 1>;
             case 4: return sim_kernel<NP, 12, 4, GEN, TC, 4>;
-            case 6: return sim_kernel<NP, 12, 4, GEN, TC, 6>;
-            default: break;
+            case 5: return sim_kernel<NP, 12, 4, GEN, TC, 5>;
+            default: return sim_kernel<NP, 12, 4, GEN, TC, 6>;
             }
         }
         return sim_kernel<NP, 12, 4, GEN, TC>;
@@ -716,7 +718,7 @@ sim_fn pick_fallback(int np, bool gen, bool tc) {
     return gen ? fb_np_gen<8, true>(tc) : fb_np_gen<8, false>(tc);
 }
 int lds_bytes(int ring, int waves) {
-    return waves * (16 * 64 * 2 + ring * 64 * 4 + 128 * 4 + 64 * 2 + K_N * 8);
+    return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 2 + K_N * 8);
 }
 
 }  // namespace
