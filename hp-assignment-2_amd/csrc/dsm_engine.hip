@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include "dsm.h"
+#include "dsm_table.h"
 
 #define DEVI __device__ __forceinline__
 
@@ -44,8 +45,6 @@ enum : uint32_t {
     T_WBINV = 7, T_WBINT = 8, T_FLUSH = 9, T_FLINV = 10, T_EVS = 11, T_EVM = 12,
     OP_RD = 13, OP_WR = 14, OP_DUMP = 15, OP_IDLE = 16
 };
-enum : uint32_t { CM = 0, CE = 1, CS = 2, CI = 3 };   /* cacheLineState :17 */
-enum : uint32_t { DEM = 0, DS = 1, DU = 2 };          /* directoryEntryState :18 */
 
 /* ctl word: bits 0-7 pendingWriteValue, then flags */
 constexpr uint32_t C_WAIT = 1u << 8, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C_ASSERT = 1u << 11;
@@ -77,6 +76,7 @@ struct SimArgs {
     unsigned int *claim;            /* 8 shard counters, 32 words apart                     */
     uint32_t *ovf_list;             /* fast kernel: systems handed to the 256-deep re-run   */
     unsigned int *ovf_count;
+    const uint2 *table;             /* micro-op table (dsm_table.h), DT_ENTRIES entries     */
 };
 
 /* ---- small bit-field helpers ------------------------------------------------------- */
@@ -98,12 +98,8 @@ DEVI uint32_t set2(uint32_t w, uint32_t i, uint32_t v) {
 }
 
 /* message body: type[0:3] addr[4:10] payload[11:18] r2[19:21] excl[22];
- * ring entry = body | sender << 23; outbox word = body | destination mask << 24 */
-DEVI uint32_t mbody(uint32_t type, uint32_t addr, uint32_t payload = 0, uint32_t r2 = 0,
-                    uint32_t excl = 0) {
-    return type | (addr << 4) | (payload << 11) | (r2 << 19) | (excl << 22);
-}
-DEVI uint32_t to(uint32_t body, uint32_t dest) { return body | (1u << (24 + dest)); }
+ * ring entry = body | sender << 23; outbox word = body | destination mask << 24
+ * (built by dt_apply, dsm_table.h) */
 
 /* ---- hashing / generator (definitions in DESIGN.md; pinned by tests) ----------------- */
 DEVI uint64_t fmix64(uint64_t z) {
@@ -234,10 +230,13 @@ sim_kernel(const SimArgs *Ap) {
     __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][128]; /* 2 words/lane  */
     __shared__ __attribute__((aligned(16))) uint16_t s_dm[WAVES][64];   /* dest masks    */
     __shared__ unsigned long long s_cnt[WAVES][K_N];
+    __shared__ uint2 s_tab[DT_ENTRIES];                                /* micro-op table */
 
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t node = lane % NP, gbase = lane - node;
     if (lane < K_N) s_cnt[wv][lane] = 0;
+    for (uint32_t i = threadIdx.x; i < DT_ENTRIES; i += 64 * WAVES) s_tab[i] = Ap->table[i];
+    __syncthreads();
 
     const uint64_t n = Ap->d_n ? (uint64_t)*Ap->d_n : Ap->n_sys;
     const uint32_t *list = Ap->list;
@@ -328,109 +327,33 @@ sim_kernel(const SimArgs *Ap) {
         }
         const uint32_t op = (hasMsg || doIssue) ? (w & 15u) : doDump ? OP_DUMP : OP_IDLE;
 
-        /* ---- (2) decode + the line / directory entry / memory byte it touches -------- */
-        const uint32_t a = (w >> 4) & 0x7Fu, v = (w >> 11) & 0xFFu, r2 = (w >> 19) & 7u;
-        const uint32_t s = (w >> 23) & 7u;
-        const uint32_t H = a >> 4, blk = a & 15u, idx = a & 3u;          /* :177-184 */
-        const uint32_t La = get8(nd.caddr, idx), Lv = get8(nd.cval, idx), Ls = get2(nd.cst, idx);
+        /* ---- (2) decode, then the micro-op table (dsm_table.h) ------------------------ */
+        const uint32_t a = (w >> 4) & 0x7Fu, blk = a & 15u, idx = a & 3u;  /* :177-184 */
         uint16_t *const mbp = reinterpret_cast<uint16_t *>(&s_mb[wv][blk >> 1][lane]) + (blk & 1u);
         const uint32_t mbw = *mbp;
-        const uint32_t Mv = mbw & 0xFFu, Db = mbw >> 8, Ds = get2(nd.dst, blk);
-        const uint32_t pend = nd.ctl & 0xFFu;
-
-        const bool home = (H == node), atR2 = (node == r2);
-        const bool hit = (La == a), valid = (Ls != CI), hitv = hit && valid;
-        const uint32_t sbit = 1u << s;
-        const bool sSet = (Db & sbit) != 0u;
-        const uint32_t ob = Db & NPM;
-        const uint32_t own = __builtin_ctz(ob | 0x80000000u);            /* findOwner :98 */
-        const bool fwd = (Ds == DEM) && (own != s);      /* owner elsewhere: forward */
-        const bool isIssue = (op == OP_RD || op == OP_WR) && H < (uint32_t)NP;
-
-        /* reference asserts (:189-190,:213,:299-300,:376-377,:408,:443,:489,:542-543) */
-        const bool lineOK = hit || La == 0xFFu || !valid;
-        const bool emNoOwner = (Ds == DEM) && ob == 0u;
-        const bool asrt = ((op == T_RREQ || op == T_WREQ || op == T_UPG || op == T_EVM) && !home) ||
-                          ((op == T_RREQ || op == T_WREQ) && emNoOwner) ||
-                          (op == T_RWR && !lineOK) || (op == T_FLINV && atR2 && !lineOK) ||
-                          ((op == OP_RD || op == OP_WR) && H >= (uint32_t)NP);
-        const bool okHome = home && !emNoOwner;
-
-        /* memory byte: WRITE_REQUEST :379, FLUSH :276, FLUSH_INVACK :478, EVICT_MODIFIED :544 */
-        const bool wMem = home && (op == T_WREQ || op == T_FLUSH || op == T_FLINV || op == T_EVM);
-        const uint32_t nMv = wMem ? v : Mv;
-
-        /* directory entry */
-        const uint32_t evDb = Db & ~sbit;
-        const uint32_t rem = __builtin_popcount(evDb & NPM);
-        uint32_t nDb = Db, nDs = Ds, o0 = 0;
-        if (op == T_RREQ && okHome) {                                    /* :196-234 */
-            nDb = (Ds == DU) ? sbit : (Db | sbit);
-            nDs = (Ds == DS || fwd) ? DS : DEM;
-            o0 = fwd ? to(mbody(T_WBINT, a, 0, s), own)
-                     : to(mbody(T_RRD, a, Mv, 0, Ds != DS ? 1u : 0u), s);
-        }
-        if (op == T_WREQ && okHome) {                                    /* :381-433 */
-            nDb = sbit; nDs = DEM;
-            o0 = fwd ? to(mbody(T_WBINV, a, 0, s), own)
-                     : (Ds == DS) ? to(mbody(T_RID, a, Db & ~sbit & 0xFFu), s)
-                                  : to(mbody(T_RWR, a), s);
-        }
-        if (op == T_UPG && home) {                                       /* :302-327 */
-            nDb = sbit; nDs = DEM;
-            o0 = to(mbody(T_RID, a, (Ds == DS) ? (Db & ~sbit & 0xFFu) : 0u), s);
-        }
-        if (op == T_FLINV && home) { nDb = 1u << r2; nDs = DEM; }        /* :479-480 */
-        if (op == T_EVS && home && sSet) {                               /* :501-521 */
-            nDb = evDb;
-            nDs = (rem == 0) ? DU : (rem == 1 && Ds == DS) ? DEM : Ds;
-            if (rem == 1 && Ds == DS) o0 = to(mbody(T_EVS, a), __builtin_ctz((evDb & NPM) | 0x80000000u));
-        }
-        if (op == T_EVM && home && Ds == DEM && sSet) { nDb = 0; nDs = DU; } /* :545-547 */
-
-        /* cache side: flush forwards, INV fan-out, victim, request */
-        const bool flushOut = (op == T_WBINT || op == T_WBINV) && hit && Ls <= CE; /* :251, :453 */
-        if (flushOut)
-            o0 = mbody(op == T_WBINT ? T_FLUSH : T_FLINV, a, Lv, r2) | (1u << (24 + H)) | (1u << (24 + r2));
-        const uint32_t invm = v & NPM & ~(1u << node);                   /* :350-362 */
-        if (op == T_RID && hit && invm) o0 = mbody(T_INV, a) | (invm << 24);
-        const bool installRd = op == T_RRD || (op == T_FLUSH && atR2);   /* :238-247, :286-295 */
-        const bool evict = (La != 0xFFu) && valid && ((installRd && !hit) || (isIssue && !hitv));
-        if (evict)                                                       /* :742-773 */
-            o0 = to((Ls == CM) ? mbody(T_EVM, La, Lv) : mbody(T_EVS, La), La >> 4);
-        const bool sendReq = isIssue && (!hitv || (op == OP_WR && Ls == CS)); /* :612-684 */
-        const uint32_t o1 = sendReq ? to(mbody(op == OP_RD ? T_RREQ : (hitv ? T_UPG : T_WREQ), a,
-                                               (op == OP_WR && !hitv) ? v : 0u), H) : 0u;
-
-        /* cache line */
-        const bool installWr = (op == T_RWR || (op == T_FLINV && atR2)) && lineOK; /* :437-495 */
-        const bool issueMiss = isIssue && !hitv;
-        const bool wrHit = op == OP_WR && isIssue && hitv;                /* :640-659 */
-        const bool ridUp = op == T_RID && hit && Ls != CM;                /* :332-336 */
-        uint32_t nLa = La, nLv = Lv, nLs = Ls;
-        if (op == T_EVS && !home && s == H && hit && Ls == CS) nLs = CE;  /* :526-532 */
-        if (op == T_INV && hit && (Ls == CS || Ls == CE)) nLs = CI;       /* :366-373 */
-        if (flushOut) nLs = (op == T_WBINT) ? CS : CI;
-        if (ridUp) { nLv = pend; nLs = CM; }
-        if (wrHit) { nLv = v; nLs = CM; }
-        if (issueMiss) { nLa = a; nLv = 0; nLs = CI; }
-        if (installWr) { nLa = a; nLv = (op == T_RWR) ? pend : v; nLs = CM; }
-        if (installRd) { nLa = a; nLv = v; nLs = (op == T_RRD && ((w >> 22) & 1u)) ? CE : CS; }
-
-        /* waitingForReply / pendingWriteValue / assert flag */
-        uint32_t ctl = nd.ctl;
-        ctl = (installRd || installWr || op == T_RID) ? (ctl & ~C_WAIT) : ctl;
-        ctl = sendReq ? (ctl | C_WAIT) : ctl;
-        ctl = (op == OP_WR && isIssue) ? ((ctl & ~0xFFu) | v) : ctl;     /* :633 */
-        ctl = asrt ? (ctl | C_ASSERT) : ctl;
-        nd.ctl = ctl;
+        DtIn in;
+        in.op = op; in.a = a; in.v = (w >> 11) & 0xFFu; in.r2 = (w >> 19) & 7u;
+        in.s = (w >> 23) & 7u; in.excl = (w >> 22) & 1u; in.node = node; in.np_mask = NPM;
+        in.La = get8(nd.caddr, idx); in.Lv = get8(nd.cval, idx); in.Ls = get2(nd.cst, idx);
+        in.Db = mbw >> 8; in.Ds = get2(nd.dst, blk); in.Mv = mbw & 0xFFu; in.pend = nd.ctl & 0xFFu;
+        uint32_t evDb, own;
+        const uint32_t ti = dt_index(in, &evDb, &own);
+        const uint2 E = s_tab[ti];
+        const DtOut o = dt_apply(in, E.x, E.y, evDb, own);
+        const uint32_t o0 = o.o0, o1 = o.o1;
 
         /* ---- (3) write back (idle lanes rewrite unchanged values) ------------------- */
-        nd.caddr = set8(nd.caddr, idx, nLa);
-        nd.cval = set8(nd.cval, idx, nLv);
-        nd.cst = set2(nd.cst, idx, nLs);
-        nd.dst = set2(nd.dst, blk, nDs);
-        *mbp = (uint16_t)(nMv | (nDb << 8));
+        nd.caddr = set8(nd.caddr, idx, o.nLa);
+        nd.cval = set8(nd.cval, idx, o.nLv);
+        nd.cst = set2(nd.cst, idx, o.nLs);
+        nd.dst = set2(nd.dst, blk, o.nDs);
+        *mbp = (uint16_t)(o.nMv | (o.nDb << 8));
+        uint32_t ctl = nd.ctl;
+        ctl = o.wclr ? (ctl & ~C_WAIT) : ctl;
+        ctl = o.wset ? (ctl | C_WAIT) : ctl;
+        ctl = o.pendw ? ((ctl & ~0xFFu) | in.v) : ctl;                   /* :633 */
+        ctl = o.asrt ? (ctl | C_ASSERT) : ctl;
+        nd.ctl = ctl;
         const bool isMsg = op <= T_EVM;
         nd.nmsg += isMsg ? 1u : 0u;
         if (TC) {
@@ -680,29 +603,33 @@ __global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist, uint6
 /* ---- kernel table ------------------------------------------------------------------- */
 typedef void (*sim_fn)(const SimArgs *);
 
+/* Waves per workgroup of the fast transition kernel: the micro-op table is one copy per
+ * workgroup in LDS, so 8 waves share it (512 threads, ~52 KB LDS with ring 12: 3 groups =
+ * 6 waves per SIMD). */
+constexpr int FW = 8;
+
 /* Occupancy target of the transition kernel (amdgpu_waves_per_eu): the register budget is
  * the lever between latency hiding and spilling; DSM_OCC selects a variant for A/B runs. */
 static int occ_choice() {
     const char *e = getenv("DSM_OCC");
-    const int v = e ? atoi(e) : 6;     /* measured best on MI355X (tools/ab_occ.py) */
-    return (v == 1 || v == 4 || v == 5) ? v : 6;
+    const int v = e ? atoi(e) : 5;     /* measured on MI355X (tools/ab_occ.py) */
+    return (v == 4 || v == 6) ? v : 5;
 }
 template <int NP, bool GEN, bool TC>
 sim_fn fast_kernel(int ring) {
     switch (ring) {
-    case 4: return sim_kernel<NP, 4, 4, GEN, TC>;
-    case 8: return sim_kernel<NP, 8, 4, GEN, TC>;
-    case 16: return sim_kernel<NP, 16, 4, GEN, TC>;
+    case 4: return sim_kernel<NP, 4, FW, GEN, TC>;
+    case 8: return sim_kernel<NP, 8, FW, GEN, TC>;
+    case 16: return sim_kernel<NP, 16, FW, GEN, TC>;
     default:
         if (NP == 8 && !TC) {
             switch (occ_choice()) {
-            case 1: return sim_kernel<NP, 12, 4, GEN, TC, 1>;
-            case 4: return sim_kernel<NP, 12, 4, GEN, TC, 4>;
-            case 5: return sim_kernel<NP, 12, 4, GEN, TC, 5>;
-            default: return sim_kernel<NP, 12, 4, GEN, TC, 6>;
+            case 4: return sim_kernel<NP, 12, FW, GEN, TC, 4>;
+            case 6: return sim_kernel<NP, 12, FW, GEN, TC, 6>;
+            default: return sim_kernel<NP, 12, FW, GEN, TC, 5>;
             }
         }
-        return sim_kernel<NP, 12, 4, GEN, TC>;
+        return sim_kernel<NP, 12, FW, GEN, TC>;
     }
 }
 template <int NP, bool GEN>
@@ -718,7 +645,7 @@ sim_fn pick_fallback(int np, bool gen, bool tc) {
     return gen ? fb_np_gen<8, true>(tc) : fb_np_gen<8, false>(tc);
 }
 int lds_bytes(int ring, int waves) {
-    return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 2 + K_N * 8);
+    return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 2 + K_N * 8) + DT_ENTRIES * 8;
 }
 
 }  // namespace
@@ -746,6 +673,7 @@ struct dsm_ctx {
     dsm_sys_result *d_res;
     size_t res_cap;
     dsm_counters *d_cnt;
+    uint2 *d_table;                  /* micro-op table, built on the host at open         */
     uint4 *d_recs;                   /* [sys][node][dump, final] node records of the last run */
     size_t recs_cap;
     uint64_t recs_n;
@@ -803,9 +731,18 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
         hipMalloc((void **)&c->d_args, 2 * sizeof(SimArgs)) != hipSuccess ||
         hipHostMalloc((void **)&c->h_args, 2 * sizeof(SimArgs), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_args, hipEventDisableTiming) != hipSuccess ||
-        hipMalloc((void **)&c->d_cnt, sizeof(dsm_counters)) != hipSuccess) {
+        hipMalloc((void **)&c->d_cnt, sizeof(dsm_counters)) != hipSuccess ||
+        hipMalloc((void **)&c->d_table, DT_ENTRIES * sizeof(uint2)) != hipSuccess) {
         dsm_close(c);
         return DSM_E_DEVICE;
+    }
+    {
+        static uint32_t tab[2 * DT_ENTRIES];
+        dt_build(tab);
+        if (hipMemcpy(c->d_table, tab, sizeof tab, hipMemcpyHostToDevice) != hipSuccess) {
+            dsm_close(c);
+            return DSM_E_DEVICE;
+        }
     }
     if ((cfg->flags & DSM_F_TIMING) &&
         (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)) {
@@ -821,7 +758,7 @@ extern "C" void dsm_close(dsm_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *ptrs[] = {c->d_ctrl, c->d_args, c->d_partials, c->d_ovf_list, c->d_traces, c->d_counts,
-                    c->d_res, c->d_cnt, c->d_recs};
+                    c->d_res, c->d_cnt, c->d_recs, c->d_table};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     if (c->h_args) (void)hipHostFree(c->h_args);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -848,16 +785,16 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     const bool tc = (c->cfg.flags & DSM_F_TYPE_COUNTS) != 0;
     sim_fn fast = pick_fast(np, c->ring, gen, tc), fb = pick_fallback(np, gen, tc);
     int nb_fast = 0, nb_fb = 0;
-    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fast, (const void *)fast, 256, 0));
+    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fast, (const void *)fast, 64 * FW, 0));
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fb, (const void *)fb, 64, 0));
     if (nb_fast < 1 || nb_fb < 1) return DSM_E_DEVICE;
-    uint64_t want = (n_sys + (uint64_t)(4 * gpw) - 1) / (uint64_t)(4 * gpw);
+    uint64_t want = (n_sys + (uint64_t)(FW * gpw) - 1) / (uint64_t)(FW * gpw);
     int grid_fast = (int)((uint64_t)nb_fast * c->cus < want ? (uint64_t)nb_fast * c->cus : want);
     int grid_fb = nb_fb * c->cus;
     if (grid_fb > 1024) grid_fb = 1024;
     uint64_t dblocks = (n_sys * np + 255) / 256;
     if (dblocks > (uint64_t)c->cus * 8) dblocks = (uint64_t)c->cus * 8;
-    const size_t waves = (size_t)grid_fast * 4 + (size_t)grid_fb + (size_t)dblocks;
+    const size_t waves = (size_t)grid_fast * FW + (size_t)grid_fb + (size_t)dblocks;
     int rc;
     if ((rc = ensure(&c->d_partials, &c->partials_waves, waves * K_N))) return rc;
     if ((rc = ensure(&c->d_ovf_list, &c->ovf_cap, (size_t)n_sys))) return rc;
@@ -889,11 +826,12 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.claim = c->d_ctrl + CTRL_FAST;
     A.ovf_list = c->d_ovf_list;
     A.ovf_count = c->d_ctrl + CTRL_OVF;
+    A.table = c->d_table;
     SimArgs &B = c->h_args[1];
     B = A;
     B.d_n = c->d_ctrl + CTRL_OVF;
     B.list = c->d_ovf_list;
-    B.partials = c->d_partials + (size_t)grid_fast * 4 * K_N;
+    B.partials = c->d_partials + (size_t)grid_fast * FW * K_N;
     B.claim = c->d_ctrl + CTRL_FB;
     B.ovf_list = nullptr;
     B.ovf_count = nullptr;
@@ -901,14 +839,14 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     HIPCK(hipEventRecord(c->ev_args, st));
 
     if (c->ev0) HIPCK(hipEventRecord(c->ev0, st));
-    hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(256), 0, st, (const SimArgs *)c->d_args);
+    hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, (const SimArgs *)c->d_args);
     HIPCK(hipGetLastError());
     if (c->ev1) { HIPCK(hipEventRecord(c->ev1, st)); c->timed = 1; }
 
     hipLaunchKernelGGL(fb, dim3(grid_fb), dim3(64), 0, st, (const SimArgs *)(c->d_args + 1));
     HIPCK(hipGetLastError());
 
-    unsigned long long *dpart = c->d_partials + ((size_t)grid_fast * 4 + grid_fb) * K_N;
+    unsigned long long *dpart = c->d_partials + ((size_t)grid_fast * FW + grid_fb) * K_N;
     if (np == 4)
         hipLaunchKernelGGL(digest_kernel<4>, dim3((unsigned)dblocks), dim3(256), 0, st, n_sys,
                            (const uint4 *)c->d_recs, d_results, dpart);
@@ -922,11 +860,11 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     HIPCK(hipGetLastError());
 
     c->info.grid_blocks = grid_fast;
-    c->info.block_threads = 256;
-    c->info.waves_per_cu = nb_fast * 4;
+    c->info.block_threads = 64 * FW;
+    c->info.waves_per_cu = nb_fast * FW;
     c->info.cus = c->cus;
     c->info.ring_cap = c->ring;
-    c->info.lds_bytes_per_block = lds_bytes(c->ring, 4);
+    c->info.lds_bytes_per_block = lds_bytes(c->ring, FW);
     return DSM_OK;
 }
 
