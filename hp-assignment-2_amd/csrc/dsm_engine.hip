@@ -202,7 +202,14 @@ DEVI uint64_t gsum64(uint64_t x) {
     }
     return x;
 }
-DEVI uint4 ld16(const uint16_t *p) { return *reinterpret_cast<const uint4 *>(p); }
+/* 16-byte trace chunk load through the global address space: a generic (flat) load is
+ * counted in both vmcnt and lgkmcnt and completes out of order, so every later wait on it,
+ * or on any LDS access, becomes vmcnt(0) lgkmcnt(0). */
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+DEVI uint4 ld16(const uint16_t *p) {
+    const v4u32 v = *(const __attribute__((address_space(1))) v4u32 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 /* gather bit `r` of each of the 4 bytes of x into bits 0..3 */
 DEVI uint32_t gather4(uint32_t x, uint32_t r) {
@@ -246,6 +253,7 @@ sim_kernel(const SimArgs *Ap) {
     const uint64_t gmul = GEN ? Ap->seed * 0x9E3779B97F4A7C15ULL : 0;
     const uint64_t gfirst = GEN ? Ap->first_sys : 0;
     const int gdist = GEN ? Ap->dist : 0;
+    const uint32_t stride = GEN ? 0u : Ap->stride;   /* >= 8, multiple of 8 (dsm_open) */
 
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
@@ -272,18 +280,15 @@ sim_kernel(const SimArgs *Ap) {
         if (GEN) {
             nd.nins = Ap->n_instr;
         } else {
-            const uint32_t stride = Ap->stride;
             const uint32_t c = Ap->counts[sys * NP + node];
             nd.nins = c < stride ? c : stride;
             tb = Ap->traces + (sys * NP + node) * (uint64_t)stride;
-            if (nd.nins > 0) {
-                const uint4 v = ld16(tb);
-                cur[0] = v.x; cur[1] = v.y; cur[2] = v.z; cur[3] = v.w;
-            }
-            if (nd.nins > 8) {
-                const uint4 v = ld16(tb + 8);
-                nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
-            }
+            /* both chunks unconditionally (in-slot), then drain them here, once per system:
+             * the round loop's only vmcnt wait is then the refill rotation */
+            const uint4 v0 = ld16(tb), v1 = ld16(tb + (stride > 8 ? 8 : 0));
+            cur[0] = v0.x; cur[1] = v0.y; cur[2] = v0.z; cur[3] = v0.w;
+            nxt[0] = v1.x; nxt[1] = v1.y; nxt[2] = v1.z; nxt[3] = v1.w;
+            __builtin_amdgcn_s_waitcnt(0x0F70);                 /* vmcnt(0) */
         }
     };
 
@@ -303,6 +308,13 @@ sim_kernel(const SimArgs *Ap) {
         const bool canIssue = live && !hasMsg && !(nd.ctl & C_WAIT);      /* :578-581 */
         const bool doIssue = canIssue && nd.ip < nd.nins;                 /* :590-592 */
         const bool doDump = canIssue && !doIssue && !(nd.ctl & C_DUMPED); /* :688-697 */
+        /* trace refill: when this round's issue takes the last instruction of `cur`, the
+         * chunk after `nxt` is requested NOW and rotated in at the end of the round, so its
+         * HBM latency overlaps this round's transition and delivery (a load consumed in the
+         * same basic block stalls the whole wave on HBM). */
+        const bool refill = !GEN && doIssue && ((nd.ip + 1) & 7u) == 0 && nd.ip + 1 < nd.nins;
+        uint4 pf;
+        if (refill) pf = ld16(tb + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
         const uint32_t headn = (head0 + 1 == (uint32_t)RING) ? 0u : head0 + 1;
         nd.rh = hasMsg ? (headn | ((cnt0 - 1) << 8)) : nd.rh;
         uint32_t w = rmsg;
@@ -316,14 +328,6 @@ sim_kernel(const SimArgs *Ap) {
             }
             w = ((ins >> 15) ? OP_WR : OP_RD) | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
             nd.ip++;
-            if (!GEN && (nd.ip & 7u) == 0 && nd.ip < nd.nins) {           /* next chunk */
-#pragma unroll
-                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-                if (nd.ip + 8 < nd.nins) {
-                    const uint4 v = ld16(tb + nd.ip + 8);
-                    nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
-                }
-            }
         }
         const uint32_t op = (hasMsg || doIssue) ? (w & 15u) : doDump ? OP_DUMP : OP_IDLE;
 
@@ -400,6 +404,11 @@ sim_kernel(const SimArgs *Ap) {
             rmsg = s_ring[wv][hh][lane];          /* next round's head, prefetched */
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        if (refill) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+            nxt[0] = pf.x; nxt[1] = pf.y; nxt[2] = pf.z; nxt[3] = pf.w;
+        }
 
         /* ---- (5) per-system termination (Appendix A step 4) -------------------------- */
         const uint64_t actb = __ballot(op != OP_IDLE);
@@ -603,38 +612,32 @@ __global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist, uint6
 /* ---- kernel table ------------------------------------------------------------------- */
 typedef void (*sim_fn)(const SimArgs *);
 
-/* Waves per workgroup of the fast transition kernel: the micro-op table is one copy per
- * workgroup in LDS, so 8 waves share it (512 threads, ~52 KB LDS with ring 12: 3 groups =
- * 6 waves per SIMD). */
-constexpr int FW = 8;
-
-/* Occupancy target of the transition kernel (amdgpu_waves_per_eu): the register budget is
- * the lever between latency hiding and spilling; DSM_OCC selects a variant for A/B runs. */
-static int occ_choice() {
-    const char *e = getenv("DSM_OCC");
-    const int v = e ? atoi(e) : 5;     /* measured on MI355X (tools/ab_occ.py) */
-    return (v == 4 || v == 6) ? v : 5;
+/* Waves per workgroup of the fast transition kernel.  The micro-op table is one copy per
+ * workgroup in LDS; at ring 12 a wave needs ~6 KB of LDS and the kernel fits 5 waves per
+ * SIMD (96 VGPRs), so 4-wave groups (5 per CU = 20 waves, 146 KB LDS) fill the CU where
+ * 8-wave groups stop at 2 per CU (16 waves).  DSM_FW=4|8 selects it for A/B runs. */
+struct FastK { sim_fn fn; int waves; };
+static int fw_choice() {
+    const char *e = getenv("DSM_FW");
+    const int v = e ? atoi(e) : 4;
+    return v == 8 ? 8 : 4;
 }
-template <int NP, bool GEN, bool TC>
+template <int NP, bool GEN, bool TC, int W>
 sim_fn fast_kernel(int ring) {
     switch (ring) {
-    case 4: return sim_kernel<NP, 4, FW, GEN, TC>;
-    case 8: return sim_kernel<NP, 8, FW, GEN, TC>;
-    case 16: return sim_kernel<NP, 16, FW, GEN, TC>;
-    default:
-        if (NP == 8 && !TC) {
-            switch (occ_choice()) {
-            case 4: return sim_kernel<NP, 12, FW, GEN, TC, 4>;
-            case 6: return sim_kernel<NP, 12, FW, GEN, TC, 6>;
-            default: return sim_kernel<NP, 12, FW, GEN, TC, 5>;
-            }
-        }
-        return sim_kernel<NP, 12, FW, GEN, TC>;
+    case 4: return sim_kernel<NP, 4, W, GEN, TC>;
+    case 8: return sim_kernel<NP, 8, W, GEN, TC>;
+    case 16: return sim_kernel<NP, 16, W, GEN, TC>;
+    default: return sim_kernel<NP, 12, W, GEN, TC>;
     }
 }
 template <int NP, bool GEN>
-sim_fn fast_np_gen(int ring, bool tc) { return tc ? fast_kernel<NP, GEN, true>(ring) : fast_kernel<NP, GEN, false>(ring); }
-sim_fn pick_fast(int np, int ring, bool gen, bool tc) {
+FastK fast_np_gen(int ring, bool tc) {
+    if (fw_choice() == 8)
+        return {tc ? fast_kernel<NP, GEN, true, 8>(ring) : fast_kernel<NP, GEN, false, 8>(ring), 8};
+    return {tc ? fast_kernel<NP, GEN, true, 4>(ring) : fast_kernel<NP, GEN, false, 4>(ring), 4};
+}
+FastK pick_fast(int np, int ring, bool gen, bool tc) {
     if (np == 4) return gen ? fast_np_gen<4, true>(ring, tc) : fast_np_gen<4, false>(ring, tc);
     return gen ? fast_np_gen<8, true>(ring, tc) : fast_np_gen<8, false>(ring, tc);
 }
@@ -783,7 +786,9 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     HIPCK(hipSetDevice(c->device));
     const int np = c->cfg.np, gpw = 64 / np;
     const bool tc = (c->cfg.flags & DSM_F_TYPE_COUNTS) != 0;
-    sim_fn fast = pick_fast(np, c->ring, gen, tc), fb = pick_fallback(np, gen, tc);
+    const FastK fk = pick_fast(np, c->ring, gen, tc);
+    const sim_fn fast = fk.fn, fb = pick_fallback(np, gen, tc);
+    const int FW = fk.waves;
     int nb_fast = 0, nb_fb = 0;
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fast, (const void *)fast, 64 * FW, 0));
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fb, (const void *)fb, 64, 0));

@@ -1,18 +1,24 @@
 #!/usr/bin/env python3
-"""tools/ab_occ.py -- interleaved in-process A/B of transition-kernel variants (DSM_OCC)
-on the bench workload (C3, traces resident in HBM).  Prints per-variant kernel ms."""
+"""tools/ab_env.py -- interleaved in-process A/B of transition-kernel variants selected by an
+environment variable read at launch time (e.g. DSM_FW=4|8), on a bench workload with traces
+resident in HBM.  Checks that every variant produces the same counters and hashes.
+
+    python tools/ab_env.py DSM_FW 4,8 [n_systems] [reps] [dist]
+"""
 import os
 import sys
+
 import numpy as np
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "hp-assignment-2_amd"))
 import pydsm  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
-variants = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "4", "5", "6"])]
-reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-dist = sys.argv[4] if len(sys.argv) > 4 else "uniform"
+var = sys.argv[1]
+variants = sys.argv[2].split(",")
+n = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
+reps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+dist = sys.argv[5] if len(sys.argv) > 5 else "uniform"
 dev = torch.device("cuda", 0)
 st = torch.cuda.current_stream(dev).cuda_stream
 eng = pydsm.Engine(8, 4096, timing=True)
@@ -22,10 +28,11 @@ out = torch.empty((n, 4), dtype=torch.int64, device=dev)
 cnt = torch.zeros(32, dtype=torch.int64, device=dev)
 eng.generate_device(dist, 1, 4096, 0, n, tr.data_ptr(), cn.data_ptr(), st)
 res = {v: [] for v in variants}
+info = {}
 ref = None
 for r in range(reps):
     for v in variants:
-        os.environ["DSM_OCC"] = str(v)
+        os.environ[var] = v
         cnt.zero_()
         eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
         ms = eng.last_kernel_ms()
@@ -35,6 +42,8 @@ for r in range(reps):
         ref = ref or key
         assert key == ref, (v, key, ref)
         res[v].append(ms)
+        info[v] = eng.launch_info()
 for v in variants:
-    print(f"DSM_OCC={v}: kernel ms median {np.median(res[v]):.2f} min {min(res[v]):.2f}  "
-          f"msgs/s {ref[0] / (np.median(res[v]) * 1e-3):.3e}  launch {eng.launch_info()['waves_per_cu']}")
+    print(f"{var}={v} [{dist}, {n} systems]: kernel ms median {np.median(res[v]):.2f} "
+          f"min {min(res[v]):.2f}  transactions/s {ref[0] / (np.median(res[v]) * 1e-3):.3e}  "
+          f"launch {info[v]}", flush=True)
