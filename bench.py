@@ -100,6 +100,7 @@ def main():
                     help="generate instructions inside the transition kernel (no HBM traces)")
     ap.add_argument("--cpu-sample", type=int, default=262144)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-dump", action="store_true", help="skip the GPU dump-formatter phase")
     args = ap.parse_args()
 
     import torch
@@ -173,6 +174,32 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
+    # printProcessorState of every node's final record, formatted on the GPU (fmt_kernel):
+    # the dump/checksum writer phase, HBM-write-bound; timed separately, not part of `value`
+    dump_stream = None
+    if not args.no_dump:
+        n_rec = n_sys * NP
+        d_txt = torch.empty(n_rec * pydsm.DUMP_SLOT, dtype=torch.uint8, device=dev)
+        d_len = torch.empty(n_rec, dtype=torch.int32, device=dev)
+        eng.format_run_dumps_device(pydsm.VIEW_FINAL, 0, n_sys, d_txt.data_ptr(), d_len.data_ptr(), sp)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 3
+        e0.record(stream)
+        for _ in range(reps):
+            eng.format_run_dumps_device(pydsm.VIEW_FINAL, 0, n_sys, d_txt.data_ptr(),
+                                        d_len.data_ptr(), sp)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        fms = e0.elapsed_time(e1) / reps
+        fbytes = n_rec * (64 + pydsm.DUMP_SLOT + 4)
+        text_bytes = int(d_len.sum().item())
+        dump_stream = dict(kernel="fmt_kernel (printProcessorState text of every final node record)",
+                           records=n_rec, text_bytes=text_bytes, bytes=fbytes, ms=round(fms, 3),
+                           per_unit="64 B record read + %d B slot + 4 B length written per node" % pydsm.DUMP_SLOT,
+                           achieved_gbs=round(fbytes / fms / 1e6, 1), peak_gbs=HBM_PEAK_GBS,
+                           frac=round(fbytes / fms / 1e6 / HBM_PEAK_GBS, 4))
+        del d_txt, d_len
+
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -223,6 +250,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "trace_stream": trace_stream,
+            "dump_stream": dump_stream,
             "systems_per_s": round(c["systems"] * K / elapsed_max, 1),
             "instructions_per_s": round(c["instrs"] * K / elapsed_max, 1),
             "counters": {k: c[k] for k in ("msgs", "instrs", "rounds", "systems", "max_rounds",

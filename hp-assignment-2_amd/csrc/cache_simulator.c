@@ -92,14 +92,11 @@ int main(int argc, char **argv) {
         return EXIT_FAILURE;
     }
     const uint32_t status = res.status & 0xFFu, dumped = res.status >> 8;
-    for (int n = 0; n < np; ++n) {
-        if (!((dumped >> n) & 1u)) continue;
-        dsm_node_state st;
-        if ((rc = dsm_get_node_state(ctx, 0, n, &st, NULL)) || (rc = dsm_write_dump(n, &st, NULL))) {
-            fprintf(stderr, "Error: dump of node %d: %s\n", n, dsm_strerror(rc));
-            dsm_close(ctx);
-            return EXIT_FAILURE;
-        }
+    /* printProcessorState of every node that finished issuing (:695), formatted on the GPU */
+    if ((rc = dsm_write_run_dumps(ctx, 0, dumped, NULL))) {
+        fprintf(stderr, "Error: dumps: %s\n", dsm_strerror(rc));
+        dsm_close(ctx);
+        return EXIT_FAILURE;
     }
     dsm_close(ctx);
     free(traces);

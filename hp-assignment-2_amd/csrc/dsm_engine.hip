@@ -34,27 +34,7 @@
 
 #include "dsm.h"
 #include "dsm_table.h"
-
-#define DEVI __device__ __forceinline__
-
-namespace {
-
-/* transactionType (assignment.c:20-34) plus the local actions of one round */
-enum : uint32_t {
-    T_RREQ = 0, T_WREQ = 1, T_RRD = 2, T_RWR = 3, T_RID = 4, T_INV = 5, T_UPG = 6,
-    T_WBINV = 7, T_WBINT = 8, T_FLUSH = 9, T_FLINV = 10, T_EVS = 11, T_EVM = 12,
-    OP_RD = 13, OP_WR = 14, OP_DUMP = 15, OP_IDLE = 16
-};
-
-/* ctl word: bits 0-7 pendingWriteValue, then flags */
-constexpr uint32_t C_WAIT = 1u << 8, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C_ASSERT = 1u << 11;
-
-/* counter slots (dsm_counters order) */
-enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
-       K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_N = 32 };
-
-constexpr uint64_t NO_SYS = ~0ull;
-constexpr int FB_RING = 256;        /* MSG_BUFFER_SIZE, assignment.c:12 */
+#include "dsm_internal.h"
 
 /* Kernel arguments live in device memory (not the kernarg segment): the hot loop needs
  * almost none of them, and loads from a plain global pointer are not hoisted into SGPRs
@@ -78,6 +58,28 @@ struct SimArgs {
     unsigned int *ovf_count;
     const uint2 *table;             /* micro-op table (dsm_table.h), DT_ENTRIES entries     */
 };
+
+
+#define DEVI __device__ __forceinline__
+
+namespace {
+
+/* transactionType (assignment.c:20-34) plus the local actions of one round */
+enum : uint32_t {
+    T_RREQ = 0, T_WREQ = 1, T_RRD = 2, T_RWR = 3, T_RID = 4, T_INV = 5, T_UPG = 6,
+    T_WBINV = 7, T_WBINT = 8, T_FLUSH = 9, T_FLINV = 10, T_EVS = 11, T_EVM = 12,
+    OP_RD = 13, OP_WR = 14, OP_DUMP = 15, OP_IDLE = 16
+};
+
+/* ctl word: bits 0-7 pendingWriteValue, then flags */
+constexpr uint32_t C_WAIT = 1u << 8, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C_ASSERT = 1u << 11;
+
+/* counter slots (dsm_counters order) */
+enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
+       K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_N = 32 };
+
+constexpr uint64_t NO_SYS = ~0ull;
+constexpr int FB_RING = 256;        /* MSG_BUFFER_SIZE, assignment.c:12 */
 
 /* ---- small bit-field helpers ------------------------------------------------------- */
 /* Runtime selection among 4 register words, written as masks: a ?: chain over array
@@ -657,50 +659,14 @@ int lds_bytes(int ring, int waves) {
 /* C ABI                                                                                   */
 /* ====================================================================================== */
 
-struct dsm_ctx {
-    int device;
-    dsm_config cfg;
-    int ring;
-    hipStream_t stream;
-    int cus;
-    unsigned int *d_ctrl;            /* claim shards (fast, fallback) + overflow count      */
-    SimArgs *d_args;                 /* [0] fast kernel, [1] 256-deep re-run                */
-    unsigned long long *d_partials;
-    size_t partials_waves;
-    uint32_t *d_ovf_list;
-    size_t ovf_cap;
-    uint16_t *d_traces;
-    size_t traces_cap;
-    uint32_t *d_counts;
-    size_t counts_cap;
-    dsm_sys_result *d_res;
-    size_t res_cap;
-    dsm_counters *d_cnt;
-    uint2 *d_table;                  /* micro-op table, built on the host at open         */
-    uint4 *d_recs;                   /* [sys][node][dump, final] node records of the last run */
-    size_t recs_cap;
-    uint64_t recs_n;
-    SimArgs *h_args;                 /* pinned host staging for the argument blocks         */
-    hipEvent_t ev0, ev1, ev_args;
-    int timed;
-    dsm_launch_info info;
-};
 
 #define CTRL_WORDS 1024
 #define CTRL_FAST 0
 #define CTRL_FB 256
 #define CTRL_OVF 512
 
-#define HIPCK(x) do { if ((x) != hipSuccess) return DSM_E_DEVICE; } while (0)
 
-template <typename T>
-static int ensure(T **p, size_t *cap, size_t need) {
-    if (*cap >= need && *p) return DSM_OK;
-    if (*p) { (void)hipFree(*p); *p = nullptr; *cap = 0; }
-    if (hipMalloc((void **)p, need * sizeof(T)) != hipSuccess) { *p = nullptr; return DSM_E_NOMEM; }
-    *cap = need;
-    return DSM_OK;
-}
+#define ensure dsm_ensure
 
 extern "C" int dsm_device_count(int *count) {
     if (!count) return DSM_E_INVAL;
@@ -763,6 +729,7 @@ extern "C" void dsm_close(dsm_ctx *c) {
     void *ptrs[] = {c->d_ctrl, c->d_args, c->d_partials, c->d_ovf_list, c->d_traces, c->d_counts,
                     c->d_res, c->d_cnt, c->d_recs, c->d_table};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    dsm_text_release(c);
     if (c->h_args) (void)hipHostFree(c->h_args);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);

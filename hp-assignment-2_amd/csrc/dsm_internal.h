@@ -1,0 +1,66 @@
+/*
+ * dsm_internal.h -- the engine context shared by the kernel translation units of libdsm.so
+ * (dsm_engine.hip: transition engine; dsm_text.hip: trace parser and dump formatter).
+ * Not part of the ABI.
+ */
+#ifndef DSM_INTERNAL_H
+#define DSM_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+
+#include "dsm.h"
+
+struct SimArgs;   /* transition-kernel argument block (dsm_engine.hip) */
+
+struct dsm_ctx {
+    int device;
+    dsm_config cfg;
+    int ring;
+    hipStream_t stream;
+    int cus;
+    unsigned int *d_ctrl;            /* claim shards (fast, fallback) + overflow count      */
+    SimArgs *d_args;                 /* [0] fast kernel, [1] 256-deep re-run                */
+    unsigned long long *d_partials;
+    size_t partials_waves;
+    uint32_t *d_ovf_list;
+    size_t ovf_cap;
+    uint16_t *d_traces;
+    size_t traces_cap;
+    uint32_t *d_counts;
+    size_t counts_cap;
+    dsm_sys_result *d_res;
+    size_t res_cap;
+    dsm_counters *d_cnt;
+    uint2 *d_table;                  /* micro-op table, built on the host at open           */
+    uint4 *d_recs;                   /* [sys][node][dump, final] node records of the last run */
+    size_t recs_cap;
+    uint64_t recs_n;
+    SimArgs *h_args;                 /* pinned host staging for the argument blocks         */
+    hipEvent_t ev0, ev1, ev_args;
+    int timed;
+    dsm_launch_info info;
+    /* dsm_text.hip */
+    uint4 *d_dump_tpl;               /* np printProcessorState templates, DSM_DUMP_SLOT each  */
+    char *d_text_tmp;                /* small staging for host-side dump writes              */
+    uint32_t *d_len_tmp;
+    char *d_parse_buf;               /* dsm_parse_traces (host text) staging                 */
+    size_t parse_cap;
+    uint64_t *d_parse_off;
+    size_t parse_off_cap;
+};
+
+#define HIPCK(x) do { if ((x) != hipSuccess) return DSM_E_DEVICE; } while (0)
+
+/* dsm_text.hip: called by dsm_close */
+void dsm_text_release(dsm_ctx *c);
+
+template <typename T>
+static inline int dsm_ensure(T **p, size_t *cap, size_t need) {
+    if (*cap >= need && *p) return DSM_OK;
+    if (*p) { (void)hipFree(*p); *p = nullptr; *cap = 0; }
+    if (hipMalloc((void **)p, need * sizeof(T)) != hipSuccess) { *p = nullptr; return DSM_E_NOMEM; }
+    *cap = need;
+    return DSM_OK;
+}
+
+#endif

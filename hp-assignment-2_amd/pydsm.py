@@ -32,6 +32,8 @@ COUNTER_FIELDS = ([f"msgs_{t}" for t in TYPE_NAMES] +
                    "wave_rounds"] + [f"reserved{i}" for i in range(5)])
 assert len(COUNTER_FIELDS) == 32
 
+DUMP_BASE, DUMP_MAX, DUMP_SLOT = 1954, 1958, 1968
+VIEW_DUMP, VIEW_FINAL = 0, 1
 E_INVAL, E_DEVICE, E_NOMEM, E_IO, E_FORMAT, E_STATE, E_RANGE = -1, -2, -3, -4, -5, -6, -7
 
 
@@ -93,6 +95,9 @@ def lib():
             "dsm_format_dump": (i32, [i32, vp, ctypes.c_char_p, ctypes.c_size_t]),
             "dsm_write_dump": (i32, [i32, vp, ctypes.c_char_p]),
             "dsm_node_hash": (u64, [i32, vp, i32]),
+            "dsm_format_dumps_device": (i32, [vp, vp, u32, u64, vp, vp, vp]),
+            "dsm_format_run_dumps_device": (i32, [vp, i32, u64, u64, vp, vp, vp]),
+            "dsm_write_run_dumps": (i32, [vp, u64, u32, ctypes.c_char_p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -206,6 +211,24 @@ class Engine:
         _check(lib().dsm_get_node_state(self.ctx, sys, node, _ptr(d), _ptr(f)), "dsm_get_node_state")
         return d, f
 
+    # -- printProcessorState on the GPU ------------------------------------------------------
+    def format_dumps_device(self, d_states, n_states, d_text, d_len, state_stride=1, stream=0):
+        _check(lib().dsm_format_dumps_device(self.ctx, ctypes.c_void_p(d_states), state_stride,
+                                             n_states, ctypes.c_void_p(d_text),
+                                             ctypes.c_void_p(d_len), ctypes.c_void_p(stream)),
+               "dsm_format_dumps_device")
+
+    def format_run_dumps_device(self, view, first_sys, n_sys, d_text, d_len, stream=0):
+        _check(lib().dsm_format_run_dumps_device(self.ctx, view, first_sys, n_sys,
+                                                 ctypes.c_void_p(d_text), ctypes.c_void_p(d_len),
+                                                 ctypes.c_void_p(stream)),
+               "dsm_format_run_dumps_device")
+
+    def write_run_dumps(self, sys, node_mask, out_dir=None):
+        _check(lib().dsm_write_run_dumps(self.ctx, sys, node_mask,
+                                         out_dir.encode() if out_dir else None),
+               "dsm_write_run_dumps")
+
     def last_kernel_ms(self):
         ms = ctypes.c_float(0)
         _check(lib().dsm_last_kernel_ms(self.ctx, ctypes.byref(ms)), "dsm_last_kernel_ms")
@@ -234,6 +257,12 @@ def format_dump(node, rec):
     if n < 0:
         raise DsmError(n, "dsm_format_dump")
     return buf.raw[:n].decode()
+
+
+def split_dumps(text, lens):
+    """Bulk GPU dump buffer (uint8, DUMP_SLOT bytes per record) + lengths -> list of str."""
+    text = np.asarray(text, dtype=np.uint8).reshape(-1, DUMP_SLOT)
+    return [bytes(text[k, :int(n)]).decode() for k, n in enumerate(np.asarray(lens))]
 
 
 def node_hash(node, rec, nwords):

@@ -7,6 +7,9 @@
  *
  *   dsm_parse_trace_file / dsm_load_test_dir  <- initializeProcessor   assignment.c:776-822
  *   dsm_format_dump / dsm_write_dump          <- printProcessorState   assignment.c:824-876
+ *   dsm_format_dumps_device / dsm_format_run_dumps_device / dsm_write_run_dumps
+ *                                             <- printProcessorState, on the GPU, for whole
+ *                                                ensembles (byte-identical text)
  *   dsm_run_* (lock-step ensemble engine)     <- the per-node loop of main (:135-699), the
  *                                                message switch (:177-566), instruction issue
  *                                                (:590-687), handleCacheReplacement
@@ -40,6 +43,9 @@ extern "C" {
 #define DSM_MAX_INSTR 4096       /* longest per-node trace the engine accepts               */
 #define DSM_NTYPES 13            /* transactionType assignment.c:20-34                     */
 #define DSM_MAX_ROUNDS (1u << 22)  /* active rounds before DSM_ROUND_LIMIT is reported */
+#define DSM_DUMP_BASE 1954       /* printProcessorState text length with no EXCLUSIVE line    */
+#define DSM_DUMP_MAX 1958        /* ... with four ("%8s" of "EXCLUSIVE" is 9 characters)       */
+#define DSM_DUMP_SLOT 1968       /* bytes per record in GPU-formatted dump buffers (16 | slot) */
 
 /* return codes */
 enum {
@@ -71,6 +77,10 @@ enum {
 
 /* synthetic address distributions (BASELINE.json configs) */
 enum { DSM_DIST_UNIFORM = 0, DSM_DIST_HOT = 1, DSM_DIST_EVICT = 2 };
+
+/* node-record views of a run (dsm_format_run_dumps_device) */
+enum { DSM_VIEW_DUMP = 0,   /* snapshot when the node finished issuing (:695)              */
+       DSM_VIEW_FINAL = 1   /* state when the system stopped                               */ };
 
 /* config flags */
 #define DSM_F_SNAPSHOTS 1u  /* keep per-node dump + final records of the last run          */
@@ -191,6 +201,19 @@ int dsm_get_node_state(dsm_ctx *ctx, uint64_t sys, int node, dsm_node_state *dum
  * recorded on the run's own stream right before and after the kernel launch.  Waits for
  * the stop event. */
 int dsm_last_kernel_ms(dsm_ctx *ctx, float *ms);
+
+/* ---- printProcessorState on the GPU (:824-876) ------------------------------------- *
+ * Text of record k goes to d_text + k * DSM_DUMP_SLOT (16-byte aligned buffer), its length
+ * (DSM_DUMP_BASE .. DSM_DUMP_MAX) to d_len[k]; the bytes after it in the slot are zero.  The
+ * node id printed for record k is k % np.  Asynchronous on `stream`. */
+int dsm_format_dumps_device(dsm_ctx *ctx, const dsm_node_state *d_states, uint32_t state_stride,
+                            uint64_t n_states, char *d_text, uint32_t *d_len, void *stream);
+/* the same for the np records of systems first_sys .. first_sys+n_sys-1 of the last run */
+int dsm_format_run_dumps_device(dsm_ctx *ctx, int view, uint64_t first_sys, uint64_t n_sys,
+                                char *d_text, uint32_t *d_len, void *stream);
+/* GPU-format the dump records of system `sys` of the last run (needs DSM_F_SNAPSHOTS) and
+ * write core_<n>_output.txt (:831) for every node n in node_mask into `dir` (NULL = CWD). */
+int dsm_write_run_dumps(dsm_ctx *ctx, uint64_t sys, uint32_t node_mask, const char *dir);
 
 /* ---- boundary helpers (host only; no GPU needed) ----------------------------------- */
 /* initializeProcessor's parser (:802-818): 20-byte fgets chunks, "RD %hhx" / "WR %hhx %hhu"

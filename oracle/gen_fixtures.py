@@ -24,6 +24,12 @@ outputs.  Nothing written here is reference source text.
   tests/golden/ensemble/<name>_recs.npy        first 16 systems' dump + final node records
                                                uint8 [16, 2, np, 64]
   tests/golden/ensemble/meta.json              generator parameters per fixture
+  tests/golden/dumps/random_recs.npy           4096 seeded random node records (uint8 [n, 64],
+                                               every field in its valid range; record k is
+                                               node k % 8)
+  tests/golden/dumps/random_md5.json           md5 + length of the reference's OWN
+                                               printProcessorState text of each of them
+                                               (oracle/_ref/ref_lockstep_np8 fmt)
 """
 import concurrent.futures as cf
 import hashlib
@@ -159,11 +165,47 @@ def ensemble():
         json.dump(meta, f, indent=1, sort_keys=True)
 
 
+def random_records(n, seed):
+    """Node records with every field in its valid range; cache states uniform over the four
+    (so about a quarter of the cache lines print the 9-character "EXCLUSIVE")."""
+    rng = np.random.default_rng(seed)
+    r = np.zeros((n, 64), dtype=np.uint8)
+    r[:, 0:16] = rng.integers(0, 256, (n, 16))          # memory
+    r[:, 16:32] = rng.integers(0, 256, (n, 16))         # directory bitVector
+    r[:, 32:48] = rng.integers(0, 3, (n, 16))           # directory state EM/S/U
+    r[:, 48:52] = rng.integers(0, 256, (n, 4))          # cache address
+    r[:, 52:56] = rng.integers(0, 256, (n, 4))          # cache value
+    r[:, 56:60] = rng.integers(0, 4, (n, 4))            # cache state
+    r[:, 60] = rng.integers(0, 256, n)                  # pendingWriteValue (not printed)
+    return r
+
+
+def dumps():
+    d = os.path.join(GOLD, "dumps")
+    os.makedirs(d, exist_ok=True)
+    recs = random_records(4096, 20261016)
+    with tempfile.TemporaryDirectory() as tmp:
+        rin, rout = os.path.join(tmp, "r.bin"), os.path.join(tmp, "t.bin")
+        recs.tofile(rin)
+        subprocess.run([os.path.join(REFBIN, "ref_lockstep_np8"), "fmt", rin, rout], check=True)
+        blob = open(rout, "rb").read()
+    out, off = [], 0
+    while off < len(blob):
+        n = int.from_bytes(blob[off:off + 4], "little")
+        out.append(dict(len=n, md5=md5(blob[off + 4:off + 4 + n])))
+        off += 4 + n
+    assert len(out) == len(recs)
+    np.save(os.path.join(d, "random_recs.npy"), recs)
+    with open(os.path.join(d, "random_md5.json"), "w") as f:
+        json.dump({"producer": "oracle/_ref/ref_lockstep_np8 fmt (assignment.c:824-876)",
+                   "np": 8, "texts": out}, f, indent=0)
+
+
 if __name__ == "__main__":
     if not os.path.exists(os.path.join(REF, "assignment.c")) or \
             not os.path.exists(os.path.join(REFBIN, "ref_lockstep_np8")):
         sys.exit("gen_fixtures: needs /root/reference and oracle/_ref (make -C oracle ref)")
-    steps = sys.argv[1:] or ["inputs", "lockstep", "observed", "ensemble"]
+    steps = sys.argv[1:] or ["inputs", "lockstep", "observed", "ensemble", "dumps"]
     for s in steps:
         print("gen_fixtures:", s, flush=True)
         globals()[s]()

@@ -21,6 +21,7 @@
  *   ref_lockstep tests <name> <out.bin>      (CWD must contain tests/<name>/core_n.txt;
  *                                            dumps written to CWD by printProcessorState)
  *   ref_lockstep gen <dist> <seed> <n_instr> <first_sys> <n_sys> <out.bin>
+ *   ref_lockstep fmt <recs.bin> <out.bin>   (printProcessorState of 64-byte records)
  * out.bin: per system one dsm_res, then NUM_PROCS dump records, then NUM_PROCS final records.
  */
 #include <stdio.h>
@@ -260,6 +261,47 @@ int main(int argc, char **argv) {
         rmdir("tests/empty"); rmdir("tests"); if (chdir("/")) {} rmdir(tmpl);
         return 0;
     }
-    fprintf(stderr, "usage: %s tests <name> <out.bin> | gen <dist> <seed> <n_instr> <first> <n> <out.bin>\n", argv[0]);
+    if (argc == 4 && !strcmp(argv[1], "fmt")) {
+        /* printProcessorState (:824-876) of each 64-byte record of argv[2]; record k is node
+         * k % NUM_PROCS.  The reference writes core_<id>_output.txt into the CWD: run in a
+         * scratch directory and append each file (u32 length + bytes) to argv[3]. */
+        FILE *in = fopen(argv[2], "rb"), *out = fopen(argv[3], "wb");
+        if (!in || !out) { perror("open"); return 1; }
+        char tmpl[] = "/tmp/reffmtXXXXXX";
+        if (!mkdtemp(tmpl) || chdir(tmpl)) { perror("scratch"); return 1; }
+        dsm_rec r;
+        static char buf[8192];
+        for (uint64_t k = 0; fread(&r, sizeof r, 1, in) == 1; ++k) {
+            processorNode nd;
+            memset(&nd, 0, sizeof nd);
+            for (int i = 0; i < MEM_SIZE; ++i) {
+                nd.memory[i] = r.memory[i];
+                nd.directory[i].bitVector = r.dir_bv[i];
+                nd.directory[i].state = (directoryEntryState)r.dir_state[i];
+            }
+            for (int i = 0; i < CACHE_SIZE; ++i) {
+                nd.cache[i].address = r.cache_addr[i];
+                nd.cache[i].value = r.cache_value[i];
+                nd.cache[i].state = (cacheLineState)r.cache_state[i];
+            }
+            const int id = (int)(k % NUM_PROCS);
+            printProcessorState(id, nd);
+            char p[64];
+            snprintf(p, sizeof p, "core_%d_output.txt", id);
+            FILE *f = fopen(p, "rb");
+            if (!f) { perror("dump"); return 1; }
+            uint32_t n = (uint32_t)fread(buf, 1, sizeof buf, f);
+            fclose(f);
+            unlink(p);
+            fwrite(&n, sizeof n, 1, out);
+            fwrite(buf, 1, n, out);
+        }
+        fclose(in);
+        fclose(out);
+        if (chdir("/")) {}
+        rmdir(tmpl);
+        return 0;
+    }
+    fprintf(stderr, "usage: %s tests <name> <out.bin> | gen <dist> <seed> <n_instr> <first> <n> <out.bin> | fmt <recs.bin> <out.bin>\n", argv[0]);
     return 2;
 }
