@@ -101,6 +101,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=262144)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dump", action="store_true", help="skip the GPU dump-formatter phase")
+    ap.add_argument("--parse-systems", type=int, default=65536,
+                    help="systems whose core files are generated as text and GPU-parsed (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -173,6 +175,43 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+
+    # initializeProcessor's reader on the GPU (parse_kernel): the same workload's core files as
+    # text (shipped-test format) for the first --parse-systems systems, scanned back into packed
+    # traces; timed separately, not part of `value`; checked bit-exact against gen_kernel
+    trace_parse = None
+    if args.parse_systems and not args.fused:
+        ps = min(args.parse_systems, n_sys)
+        off = torch.zeros(ps * NP + 1, dtype=torch.int64, device=dev)
+        eng.generate_text_device(dname, seed, n_instr, first, ps, 0, off.data_ptr(), sp)
+        torch.cuda.synchronize(dev)
+        tbytes = int(off[-1].item())
+        txt = torch.empty(tbytes + 64, dtype=torch.uint8, device=dev)
+        eng.generate_text_device(dname, seed, n_instr, first, ps, txt.data_ptr(), off.data_ptr(), sp)
+        ptr = torch.empty((ps, NP, n_instr), dtype=torch.int16, device=dev)
+        pcn = torch.empty((ps, NP), dtype=torch.int32, device=dev)
+        pst = torch.empty((ps, NP), dtype=torch.int32, device=dev)
+        eng.parse_traces_device(txt.data_ptr(), off.data_ptr(), ps * NP, n_instr, ptr.data_ptr(),
+                                pcn.data_ptr(), pst.data_ptr(), sp)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 3
+        e0.record(stream)
+        for _ in range(reps):
+            eng.parse_traces_device(txt.data_ptr(), off.data_ptr(), ps * NP, n_instr,
+                                    ptr.data_ptr(), pcn.data_ptr(), pst.data_ptr(), sp)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        pms = e0.elapsed_time(e1) / reps
+        ok = (int(pst.abs().sum().item()) == 0 and torch.equal(pcn, counts[:ps]) and
+              torch.equal(ptr, traces[:ps]))
+        pbytes = tbytes + ptr.numel() * 2 + pcn.numel() * 4 + off.numel() * 8
+        trace_parse = dict(kernel="parse_kernel (core_n.txt text -> packed traces, fgets/sscanf semantics)",
+                           systems=ps, text_bytes=tbytes, bytes=pbytes, ms=round(pms, 3),
+                           per_unit="text bytes read + 2 B per packed instruction + 4 B count + 8 B offset per file written/read",
+                           achieved_gbs=round(pbytes / pms / 1e6, 1), peak_gbs=HBM_PEAK_GBS,
+                           frac=round(pbytes / pms / 1e6 / HBM_PEAK_GBS, 4),
+                           parity="bit-exact vs gen_kernel traces" if ok else "MISMATCH")
+        del txt, ptr, pcn, pst, off
 
     # printProcessorState of every node's final record, formatted on the GPU (fmt_kernel):
     # the dump/checksum writer phase, HBM-write-bound; timed separately, not part of `value`
@@ -250,6 +289,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "trace_stream": trace_stream,
+            "trace_parse": trace_parse,
             "dump_stream": dump_stream,
             "systems_per_s": round(c["systems"] * K / elapsed_max, 1),
             "instructions_per_s": round(c["instrs"] * K / elapsed_max, 1),

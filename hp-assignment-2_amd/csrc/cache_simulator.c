@@ -4,10 +4,11 @@
  *
  *     ./cache_simulator <test_directory>
  *
- * reads tests/<test_directory>/core_<n>.txt relative to the CWD (:794), prints
- * "Processor <n> initialized" per node (:821), simulates the system on the GPU through
- * libdsm.so under the deterministic lock-step schedule, and writes the printProcessorState
- * dump core_<n>_output.txt (:824-876) of every node that finished issuing, into the CWD.
+ * reads tests/<test_directory>/core_<n>.txt relative to the CWD (:794) and scans them on the
+ * GPU (initializeProcessor's fgets/sscanf semantics), prints "Processor <n> initialized" per
+ * node (:821), simulates the system on the GPU through libdsm.so under the deterministic
+ * lock-step schedule, and writes the printProcessorState dump core_<n>_output.txt
+ * (:824-876) of every node that finished issuing into the CWD, formatted on the GPU.
  *
  * Unlike the reference (whose loop never exits, :153, :584-587) it exits once the system is
  * quiescent: 0 = every node dumped, 2 = deadlocked (the stuck nodes write no dump, as in the
@@ -47,32 +48,32 @@ int main(int argc, char **argv) {
         return EXIT_FAILURE;
     }
     const uint32_t stride = (max_instr + 7u) & ~7u;
-    uint16_t *traces = (uint16_t *)calloc((size_t)np * stride, sizeof(uint16_t));
-    uint32_t counts[DSM_MAX_NP] = {0};
-    if (!traces) return EXIT_FAILURE;
-
+    /* initializeProcessor (:776-822): the core files are read from disk here and scanned on
+     * the GPU with the reference's fgets/sscanf semantics (dsm_parse_traces) */
+    char *text = NULL;
+    uint64_t off[DSM_MAX_NP + 1] = {0};
     for (int n = 0; n < np; ++n) {
         char path[256];
         snprintf(path, sizeof path, "tests/%s/core_%d.txt", dir, n);   /* :794 */
-        int rc = dsm_parse_trace_file(path, traces + (size_t)n * stride, max_instr, &counts[n]);
-        if (rc == DSM_E_IO) {                                          /* :796-800 */
+        FILE *f = fopen(path, "rb");
+        if (!f) {                                                      /* :796-800 */
             fprintf(stderr, "Error: could not open file %s\n", path);
             perror("fopen");
             exit(EXIT_FAILURE);
         }
-        if (rc) {
-            fprintf(stderr, "Error: %s: %s\n", path, dsm_strerror(rc));
-            exit(EXIT_FAILURE);
+        char buf[1 << 16];
+        size_t k;
+        uint64_t len = off[n];
+        while ((k = fread(buf, 1, sizeof buf, f)) > 0) {
+            char *t = (char *)realloc(text, len + k);
+            if (!t) { fclose(f); return EXIT_FAILURE; }
+            text = t;
+            memcpy(text + len, buf, k);
+            len += k;
         }
-        for (uint32_t i = 0; i < counts[n]; ++i)
-            if (((traces[(size_t)n * stride + i] >> 12) & 7u) >= (unsigned)np) {
-                fprintf(stderr, "Error: %s: %s\n", path, dsm_strerror(DSM_E_RANGE));
-                exit(EXIT_FAILURE);
-            }
-        if (!quiet) printf("Processor %d initialized\n", n);           /* :821 */
+        fclose(f);
+        off[n + 1] = len;
     }
-    fflush(stdout);
-
     dsm_config cfg;
     memset(&cfg, 0, sizeof cfg);
     cfg.np = np;
@@ -84,6 +85,27 @@ int main(int argc, char **argv) {
         fprintf(stderr, "Error: dsm_open: %s\n", dsm_strerror(rc));
         return EXIT_FAILURE;
     }
+
+    uint16_t *traces = (uint16_t *)calloc((size_t)np * stride, sizeof(uint16_t));
+    uint32_t counts[DSM_MAX_NP] = {0};
+    int32_t pst[DSM_MAX_NP] = {0};
+    if (!traces) return EXIT_FAILURE;
+    rc = dsm_parse_traces(ctx, text ? text : "", off, (uint64_t)np, max_instr, traces, counts, pst);
+    if (rc) {
+        fprintf(stderr, "Error: dsm_parse_traces: %s\n", dsm_strerror(rc));
+        return EXIT_FAILURE;
+    }
+    for (int n = 0; n < np; ++n) {
+        if (pst[n]) {
+            fprintf(stderr, "Error: tests/%s/core_%d.txt: %s (instruction %u)\n", dir, n,
+                    dsm_strerror(pst[n]), counts[n]);
+            exit(EXIT_FAILURE);
+        }
+        if (!quiet) printf("Processor %d initialized\n", n);           /* :821 */
+    }
+    fflush(stdout);
+    free(text);
+
     dsm_sys_result res;
     rc = dsm_run_packed(ctx, traces, counts, 1, &res, NULL);
     if (rc) {

@@ -2,9 +2,22 @@
  * dsm_text.hip -- gfx950 kernels for the two text boundaries of the reference
  * (ruubhagat/HP-Assignment-2, assignment.c), part of libdsm.so:
  *
+ *   parse_kernel initializeProcessor's trace reader (:802-818) for whole ensembles of core
+ *                files: fgets(line, 20) chunking + sscanf("RD %hhx") / sscanf("WR %hhx %hhu")
+ *                (dsm_parse.h) -> packed u16 traces + counts (HBM-read-bound).
  *   fmt_kernel   printProcessorState (:824-876) for whole ensembles: the 55-line dump of every
  *                selected node record, byte-identical to the reference's fprintf output,
  *                written into fixed DSM_DUMP_SLOT-byte slots (HBM-write-bound).
+ *   textlen_kernel / textgen_kernel / scan_kernel
+ *                synthetic core files in the shipped tests' text format, from the
+ *                counter-based generator (bench and test inputs for parse_kernel).
+ *
+ * parse_kernel: one wave per file, 1 KB windows (16 B per lane, aligned loads, staged in
+ * LDS with a 32-byte halo).  A chunk starts at each line start and every 19 bytes into a
+ * longer line; every lane finds the chunk starts among its 16 bytes (distance to the line
+ * start mod 19, the line start carried across lanes by a wave max-scan), a wave prefix sum
+ * gives each chunk its instruction index, and each lane parses its chunks from LDS.  The first
+ * failing chunk (by index) ends the file, as the reference's loop would have misbehaved there.
  *
  * Layout of one dump (Appendix C of SURVEY.md): the memory and directory sections are fixed
  * width (%3d / %02X / %5d / %2s / %08X of byte-sized fields), so only the cache section moves:
@@ -20,7 +33,9 @@
 #include <string.h>
 
 #include "dsm.h"
+#include "dsm_gen.h"
 #include "dsm_internal.h"
+#include "dsm_parse.h"
 
 #define DEVI __device__ __forceinline__
 
@@ -33,7 +48,6 @@ constexpr uint32_t SLOT = DSM_DUMP_SLOT, SLOT16 = DSM_DUMP_SLOT / 16;
 constexpr uint32_t MEM0 = 193, MEML = 31;     /* "|  %3d  |  0x%02X   |  %5d   |\n"      :846 */
 constexpr uint32_t DIR0 = 856, DIRL = 45;     /* "|  %3d  |  0x%02X   |  %2s   |   0x%08X   |\n" :856 */
 constexpr uint32_t CAC0 = 1748, CACL = 41;    /* "|  %3d  |  0x%02X   |  %3d  |  %8s \t|\n" :867 */
-constexpr uint32_t FR = 16;                   /* records per workgroup iteration (31.5 KB LDS) */
 constexpr uint32_t ITEMS = 16 + 16 + 4;       /* memory, directory, cache lines per record */
 
 DEVI char hexu(uint32_t d) { return (char)(d < 10 ? '0' + d : 'A' + d - 10); }
@@ -44,9 +58,11 @@ DEVI void dec3(char *p, uint32_t v) {
     p[2] = (char)('0' + v % 10);
 }
 
-__global__ void __launch_bounds__(256) fmt_kernel(const uint8_t *recs, uint64_t rec_stride,
-                                                  uint64_t n, int np, const uint4 *tpl,
-                                                  v4u32 *out, uint32_t *lens) {
+/* FR records per workgroup iteration, NT threads per workgroup */
+template <uint32_t FR, uint32_t NT>
+__global__ void __launch_bounds__(NT) fmt_kernel(const uint8_t *recs, uint64_t rec_stride,
+                                                 uint64_t n, int np, const uint4 *tpl,
+                                                 v4u32 *out, uint32_t *lens) {
     __shared__ uint4 s_buf[FR * SLOT16];
     __shared__ uint32_t s_rec[FR][16];
     char *const sb = reinterpret_cast<char *>(s_buf);
@@ -54,7 +70,7 @@ __global__ void __launch_bounds__(256) fmt_kernel(const uint8_t *recs, uint64_t 
     for (uint64_t base = (uint64_t)blockIdx.x * FR; base < n; base += (uint64_t)gridDim.x * FR) {
         const uint32_t nr = (n - base) < FR ? (uint32_t)(n - base) : FR;
         /* (1) node-id template (static text + node-dependent address column) and records */
-        for (uint32_t i = tid; i < nr * SLOT16; i += 256) {
+        for (uint32_t i = tid; i < nr * SLOT16; i += NT) {
             const uint32_t r = i / SLOT16, c = i - r * SLOT16;
             s_buf[i] = tpl[(uint32_t)((base + r) % (uint64_t)np) * SLOT16 + c];
         }
@@ -66,7 +82,7 @@ __global__ void __launch_bounds__(256) fmt_kernel(const uint8_t *recs, uint64_t 
         }
         __syncthreads();
         /* (2) one work item per variable field group */
-        for (uint32_t i = tid; i < nr * ITEMS; i += 256) {
+        for (uint32_t i = tid; i < nr * ITEMS; i += NT) {
             const uint32_t r = i / ITEMS, f = i - r * ITEMS;
             const uint8_t *rb = reinterpret_cast<const uint8_t *>(s_rec[r]);
             char *t = sb + r * SLOT;
@@ -111,13 +127,302 @@ __global__ void __launch_bounds__(256) fmt_kernel(const uint8_t *recs, uint64_t 
         __syncthreads();
         /* (3) stream the slots out: contiguous, 16 B per lane, written once */
         v4u32 *dst = out + base * SLOT16;
-        for (uint32_t i = tid; i < nr * SLOT16; i += 256) {
+        for (uint32_t i = tid; i < nr * SLOT16; i += NT) {
             const uint4 x = s_buf[i];
             v4u32 y;
             y.x = x.x; y.y = x.y; y.z = x.z; y.w = x.w;
             __builtin_nontemporal_store(y, dst + i);
         }
         __syncthreads();
+    }
+}
+
+
+/* ---- trace parser ------------------------------------------------------------------- */
+constexpr uint32_t PWIN = 1024, PHALO = 32, PW = 4;   /* window bytes, halo, waves/group */
+
+/* aligned 16-byte load through the global address space (in-order vmcnt, not flat) */
+DEVI uint4 ldg16(const uint8_t *p) {
+    const v4u32 v = *(const __attribute__((address_space(1))) v4u32 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+/* wave64 inclusive scans on DPP (row_shr 1/2/3/4/8, row_bcast 15/31; no LDS round trips) */
+#define DPP(x, ctrl, rm, bm, bc) __builtin_amdgcn_update_dpp(0u, (x), (ctrl), (rm), (bm), (bc))
+DEVI uint32_t wave_incl_sum(uint32_t x) {
+    uint32_t s = x + DPP(x, 0x111, 0xF, 0xF, true);
+    s += DPP(x, 0x112, 0xF, 0xF, true);
+    s += DPP(x, 0x113, 0xF, 0xF, true);
+    s += DPP(s, 0x114, 0xF, 0xE, false);
+    s += DPP(s, 0x118, 0xF, 0xC, false);
+    s += DPP(s, 0x142, 0xA, 0xF, false);
+    s += DPP(s, 0x143, 0xC, 0xF, false);
+    return s;
+}
+DEVI uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+DEVI uint32_t wave_incl_max(uint32_t x) {
+    uint32_t s = umax(x, DPP(x, 0x111, 0xF, 0xF, true));
+    s = umax(s, DPP(x, 0x112, 0xF, 0xF, true));
+    s = umax(s, DPP(x, 0x113, 0xF, 0xF, true));
+    s = umax(s, DPP(s, 0x114, 0xF, 0xE, false));
+    s = umax(s, DPP(s, 0x118, 0xF, 0xC, false));
+    s = umax(s, DPP(s, 0x142, 0xA, 0xF, false));
+    s = umax(s, DPP(s, 0x143, 0xC, 0xF, false));
+    return s;
+}
+DEVI uint32_t wave_min(uint32_t x) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_xor(x, o, 64);
+        x = t < x ? t : x;
+    }
+    return x;
+}
+
+/* ASCII helpers on one byte */
+DEVI uint32_t is_dec(uint32_t c) { return (c - '0') < 10u; }
+DEVI uint32_t hexval(uint32_t c) {            /* 0..15, or >= 16 */
+    const uint32_t lo = c | 0x20u;
+    return is_dec(c) ? c - '0' : ((lo - 'a') < 6u ? lo - 'a' + 10u : 16u);
+}
+
+/* Fast path for the canonical lines "RD 0xHH\n" and "WR 0xHH D{1,3}\n" (H hex, D decimal),
+ * read from the 12 chunk bytes in c0..c2; every other chunk takes dp_parse_chunk_at.  For
+ * those two shapes sscanf's result is exactly the one computed here (dsm_parse.h).
+ * Returns 1 and *pk when the chunk has one of the shapes (and lim admits it). */
+DEVI uint32_t parse_fast(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t lim, uint32_t *pk) {
+    const uint32_t h1 = hexval((c1 >> 8) & 0xFFu), h2 = hexval((c1 >> 16) & 0xFFu);
+    const uint32_t a = (h1 << 4) | h2;
+    const bool hexok = (c1 & 0xFFu) == 'x' && h1 < 16u && h2 < 16u && a <= 0x7Fu;  /* else slow */
+    if (c0 == 0x30204452u && hexok && (c1 >> 24) == '\n' && lim >= 8u) {        /* "RD 0x" */
+        *pk = a << 8;
+        return 1u;
+    }
+    if (c0 == 0x30205257u && hexok && (c1 >> 24) == ' ') {                        /* "WR 0x" */
+        const uint32_t b8 = c2 & 0xFFu, b9 = (c2 >> 8) & 0xFFu, b10 = (c2 >> 16) & 0xFFu,
+                       b11 = c2 >> 24;
+        uint32_t v, n;
+        if (!is_dec(b8)) return 0u;
+        if (b9 == '\n') { v = b8 - '0'; n = 10u; }
+        else if (is_dec(b9) && b10 == '\n') { v = (b8 - '0') * 10u + (b9 - '0'); n = 11u; }
+        else if (is_dec(b9) && is_dec(b10) && b11 == '\n') {
+            v = (b8 - '0') * 100u + (b9 - '0') * 10u + (b10 - '0'); n = 12u;
+        } else return 0u;
+        if (lim < n) return 0u;
+        *pk = (1u << 15) | (a << 8) | (v & 0xFFu);
+        return 1u;
+    }
+    return 0u;
+}
+
+/* One file per wave; windows double-buffered in registers (the next window's loads are in
+ * flight while this one is scanned), staged in LDS for the chunk reads. */
+__global__ void __launch_bounds__(64 * PW) parse_kernel(const uint8_t *text, const uint64_t *off,
+                                                      uint64_t n_files, uint32_t cap,
+                                                      uint32_t stride, int np, uint16_t *traces,
+                                                      uint32_t *counts, int32_t *status) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_txt[PW][PWIN + PHALO + 16];
+    __shared__ uint16_t s_list[PW][PWIN];               /* chunk offsets of the window */
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint8_t *const st = s_txt[wv];
+    uint16_t *const sl = s_list[wv];
+    for (uint64_t f = (uint64_t)blockIdx.x * PW + wv; f < n_files; f += (uint64_t)gridDim.x * PW) {
+        const uint64_t b0 = off[f], b1 = off[f + 1];
+        uint16_t *const out = traces + f * stride;
+        const uint64_t wbeg = b0 & ~15ull;
+        const uint64_t last = b1 > wbeg ? ((b1 - 1) & ~15ull) : wbeg;     /* last in-file block */
+        /* window loads: always issued (address clamped into the file) so they land straight
+         * in their registers; bytes outside the file are masked by position */
+        auto load = [&](uint64_t wa, uint4 &v, uint4 &h) {
+            const uint64_t q = wa + 16u * lane, hq = wa + PWIN + 16u * (lane & 1u);
+            v = ldg16(text + (q < last ? q : last));
+            h = ldg16(text + (hq < last ? hq : last));
+        };
+        uint32_t ls_rel = 0;          /* start of the line open at the window start, - b0   */
+        uint32_t idx0 = 0;            /* chunks before the window                           */
+        uint32_t err = 0xFFFFFFFFu;   /* first failing chunk: index * 8 + error class        */
+        uint4 va, ha, vb, hb;
+        uint64_t wa = wbeg;
+        bool more = wbeg < b1;
+        if (more) load(wa, va, ha);
+        auto window = [&](uint64_t wa, const uint4 &v, const uint4 &h) {
+            /* (1) stage [wa, wa + PWIN + PHALO) */
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            reinterpret_cast<uint4 *>(st)[lane] = v;
+            if (lane < 2) reinterpret_cast<uint4 *>(st + PWIN)[lane] = h;
+            /* (2) newlines among this lane's in-file bytes */
+            const uint64_t base = wa + 16u * lane;
+            const uint32_t lo = base < b0 ? (uint32_t)(b0 - base) : 0u;          /* < 16 */
+            const uint32_t hi = base + 16 <= b1 ? 16u : (base < b1 ? (uint32_t)(b1 - base) : 0u);
+            const uint32_t fm = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            uint32_t nl = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {                /* bytes == '\n', 4 at a time */
+                const uint32_t t = w[k] ^ 0x0A0A0A0Au;
+                const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+                nl |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
+            }
+            nl &= fm;
+            /* (3) line start at this lane's first byte: max over lower lanes of (last nl + 1) */
+            const uint32_t my = nl ? (uint32_t)(base + (31u - __builtin_clz(nl)) + 1u - b0) : 0u;
+            const uint32_t incl = wave_incl_max(my);
+            const uint32_t lsr = umax(DPP(incl, 0x138, 0xF, 0xF, true), ls_rel);  /* wave_shr:1 */
+            /* (4) chunk starts: line starts, and every 19 bytes into a longer line */
+            const uint32_t din = lo > 0 ? 0u : (uint32_t)(base - b0) - lsr;   /* distance at byte 0 */
+            const uint32_t fnl = nl ? __builtin_ctz(nl) : 15u;
+            uint32_t cs;
+            if (lo > 0 || din + (fnl < 15u ? fnl : 15u) < DP_CHUNK) {
+                cs = (((nl << 1) & 0xFFFFu) | (lo > 0 ? (1u << lo) : (din == 0 ? 1u : 0u))) & fm;
+            } else {                                     /* a line of >= 19 bytes reaches here */
+                uint32_t d = din % DP_CHUNK;
+                cs = 0;
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t in = (fm >> j) & 1u;
+                    cs |= (uint32_t)(in && d == 0) << j;
+                    d = ((nl >> j) & 1u) ? 0u : (d == DP_CHUNK - 1 ? 0u : d + in);
+                }
+            }
+            /* (5) compact the chunk starts of the window (window order = instruction order) */
+            const uint32_t nc = __builtin_popcount(cs);
+            const uint32_t isum = wave_incl_sum(nc);
+            const uint32_t T = __builtin_amdgcn_readlane(isum, 63);
+            {
+                uint32_t k = isum - nc;
+                for (uint32_t m = cs; m; m &= m - 1u) sl[k++] = (uint16_t)(16u * lane + __builtin_ctz(m));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            /* (6) one chunk per lane per round: parse from LDS, coalesced 2-byte stores */
+            const uint32_t tmax = cap - idx0 < T ? cap - idx0 : T;
+            for (uint32_t t0 = 0; t0 < tmax; t0 += 64) {
+                const uint32_t t = t0 + lane;
+                if (t < tmax) {
+                    const uint32_t o = sl[t];
+                    const uint64_t p = wa + o;
+                    const uint32_t lim = (b1 - p) < DP_CHUNK ? (uint32_t)(b1 - p) : DP_CHUNK;
+                    const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
+                    const uint32_t sh = (o & 3u) * 8u;
+                    const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
+                    const uint32_t c0 = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;
+                    const uint32_t c1 = sh ? (d1 >> sh) | (d2 << (32 - sh)) : d1;
+                    const uint32_t c2 = sh ? (d2 >> sh) | (d3 << (32 - sh)) : d2;
+                    uint32_t pk = 0;
+                    int rc = 0;
+                    if (!parse_fast(c0, c1, c2, lim, &pk)) {
+                        uint32_t len = 0;
+                        while (len < lim) { if (st[o + len++] == '\n') break; }
+                        rc = dp_parse_chunk_at([&](uint32_t i) -> uint32_t { return i < len ? (uint32_t)st[o + i] : 0u; }, &pk);
+                    }
+                    if (rc == 0 && ((pk >> 12) & 7u) >= (uint32_t)np) rc = DSM_E_RANGE;   /* home < np */
+                    if (rc == 0) out[idx0 + t] = (uint16_t)pk;
+                    else {
+                        const uint32_t e = (idx0 + t) * 8u + (rc == DSM_E_FORMAT ? 1u : 2u);
+                        err = e < err ? e : err;
+                    }
+                }
+            }
+            if (__ballot(err != 0xFFFFFFFFu)) err = wave_min(err);
+            idx0 += T;
+            ls_rel = umax(ls_rel, __builtin_amdgcn_readlane(incl, 63));
+        };
+        /* the next window's loads are unconditional (clamped): a conditional load makes the
+         * waitcnt at the join assume it was not issued, i.e. wait for it right away */
+        while (more) {
+            const uint64_t wn = wa + PWIN;
+            load(wn, vb, hb);
+            window(wa, va, ha);
+            more = wn < b1 && idx0 < cap && err == 0xFFFFFFFFu;
+            if (!more) break;
+            wa = wn;
+            const uint64_t wn2 = wa + PWIN;
+            load(wn2, va, ha);
+            window(wa, vb, hb);
+            more = wn2 < b1 && idx0 < cap && err == 0xFFFFFFFFu;
+            wa = wn2;
+        }
+        if (lane == 0) {
+            uint32_t n = idx0 < cap ? idx0 : cap;
+            int32_t sc = DSM_OK;
+            if (err != 0xFFFFFFFFu && (err >> 3) < n) {
+                n = err >> 3;
+                sc = (err & 7u) == 1u ? DSM_E_FORMAT : DSM_E_RANGE;
+            }
+            counts[f] = n;
+            if (status) status[f] = sc;
+        }
+    }
+}
+
+/* ---- synthetic core files ("RD 0x%02x\n" / "WR 0x%02x %u\n", the shipped core_n.txt format) -- */
+DEVI uint32_t text_line_len(uint32_t ins) {
+    if (!(ins >> 15)) return 8u;
+    const uint32_t v = ins & 0xFFu;
+    return 10u + (v >= 10u) + (v >= 100u);
+}
+template <int NP>
+__global__ void __launch_bounds__(256) textlen_kernel(uint64_t seed, int dist, uint64_t first,
+                                                    uint64_t n_files, uint32_t n_instr,
+                                                    uint64_t *lens) {
+    const uint64_t gmul = seed * 0x9E3779B97F4A7C15ULL;
+    for (uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x; f < n_files;
+         f += (uint64_t)gridDim.x * 256) {
+        uint64_t s = 0;
+        for (uint32_t i = 0; i < n_instr; ++i)
+            s += text_line_len(dsmg::gen_instr<NP>(gmul, dist, first + f / NP, (uint32_t)(f % NP), i));
+        lens[f + 1] = s;
+    }
+}
+/* exclusive scan of lens[1..n] into offsets (in place, offsets[0] = 0), one workgroup */
+__global__ void __launch_bounds__(1024) scan_kernel(uint64_t *a, uint64_t n) {
+    __shared__ uint64_t s[1024];
+    const uint64_t per = (n + 1023) / 1024, lo = threadIdx.x * per;
+    const uint64_t hi = lo + per < n ? lo + per : n;
+    uint64_t t = 0;
+    for (uint64_t i = lo; i < hi; ++i) t += a[i + 1];
+    s[threadIdx.x] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int i = 0; i < 1024; ++i) { const uint64_t x = s[i]; s[i] = acc; acc += x; }
+    }
+    __syncthreads();
+    uint64_t acc = s[threadIdx.x];
+    for (uint64_t i = lo; i < hi; ++i) { const uint64_t x = a[i + 1]; a[i + 1] = acc + x; acc += x; }
+    if (threadIdx.x == 0) a[0] = 0;
+}
+/* one wave per file, 64 lines per step; line bytes written one at a time (setup, not timed) */
+template <int NP>
+__global__ void __launch_bounds__(256) textgen_kernel(uint64_t seed, int dist, uint64_t first,
+                                                    uint64_t n_files, uint32_t n_instr,
+                                                    const uint64_t *off, uint8_t *text) {
+    const uint64_t gmul = seed * 0x9E3779B97F4A7C15ULL;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint64_t f = (uint64_t)blockIdx.x * 4 + wv; f < n_files; f += (uint64_t)gridDim.x * 4) {
+        uint64_t pos = off[f];
+        for (uint32_t i0 = 0; i0 < n_instr; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool ok = i < n_instr;
+            const uint32_t ins = ok ? dsmg::gen_instr<NP>(gmul, dist, first + f / NP, (uint32_t)(f % NP), i) : 0u;
+            const uint32_t len = ok ? text_line_len(ins) : 0u;
+            const uint32_t inc = wave_incl_sum(len);
+            uint8_t *q = text + pos + (inc - len);
+            if (ok) {
+                const uint32_t a = (ins >> 8) & 0x7Fu, v = ins & 0xFFu;
+                const bool wr = ins >> 15;
+                q[0] = wr ? 'W' : 'R'; q[1] = wr ? 'R' : 'D'; q[2] = ' '; q[3] = '0'; q[4] = 'x';
+                q[5] = (uint8_t)"0123456789abcdef"[a >> 4]; q[6] = (uint8_t)"0123456789abcdef"[a & 15u];
+                if (!wr) q[7] = '\n';
+                else {
+                    q[7] = ' ';
+                    uint32_t k = 8;
+                    if (v >= 100u) q[k++] = (uint8_t)('0' + v / 100u);
+                    if (v >= 10u) q[k++] = (uint8_t)('0' + (v / 10u) % 10u);
+                    q[k++] = (uint8_t)('0' + v % 10u);
+                    q[k] = '\n';
+                }
+            }
+            pos += __shfl(inc, 63, 64);
+        }
     }
 }
 
@@ -152,16 +457,35 @@ static int ensure_templates(dsm_ctx *c) {
     return DSM_OK;
 }
 
+/* Workgroup tile of fmt_kernel: DSM_FMT=16|8|4 records per iteration (256 / 128 / 64
+ * threads) for A/B runs; smaller tiles put more independent copy-patch-store pipelines on
+ * each CU. */
+static int fmt_choice() {
+    const char *e = getenv("DSM_FMT");
+    const int v = e ? atoi(e) : 16;
+    return (v == 4 || v == 8) ? v : 16;
+}
+
 static int launch_fmt(dsm_ctx *c, const uint8_t *recs, uint64_t stride_bytes, uint64_t n,
                       char *d_text, uint32_t *d_len, hipStream_t st) {
     if (n == 0) return DSM_OK;
     int rc = ensure_templates(c);
     if (rc) return rc;
-    uint64_t blocks = (n + FR - 1) / FR;
-    const uint64_t cap = (uint64_t)c->cus * 4;   /* 4 x 31.5 KB LDS per CU */
+    const int fr = fmt_choice();
+    uint64_t blocks = (n + fr - 1) / fr;
+    const uint64_t cap = (uint64_t)c->cus * (64 / fr) * 4;   /* 4 waves' worth per CU per tile size */
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL(fmt_kernel, dim3((unsigned)blocks), dim3(256), 0, st, recs, stride_bytes, n,
-                       c->cfg.np, (const uint4 *)c->d_dump_tpl, (v4u32 *)d_text, d_len);
+    const uint4 *tpl = (const uint4 *)c->d_dump_tpl;
+    v4u32 *out = (v4u32 *)d_text;
+    if (fr == 4)
+        hipLaunchKernelGGL((fmt_kernel<4, 64>), dim3((unsigned)blocks), dim3(64), 0, st, recs,
+                           stride_bytes, n, c->cfg.np, tpl, out, d_len);
+    else if (fr == 8)
+        hipLaunchKernelGGL((fmt_kernel<8, 128>), dim3((unsigned)blocks), dim3(128), 0, st, recs,
+                           stride_bytes, n, c->cfg.np, tpl, out, d_len);
+    else
+        hipLaunchKernelGGL((fmt_kernel<16, 256>), dim3((unsigned)blocks), dim3(256), 0, st, recs,
+                           stride_bytes, n, c->cfg.np, tpl, out, d_len);
     HIPCK(hipGetLastError());
     return DSM_OK;
 }
@@ -220,4 +544,99 @@ extern "C" int dsm_write_run_dumps(dsm_ctx *c, uint64_t sys, uint32_t node_mask,
     }
     free(h);
     return rc;
+}
+
+/* ---- trace parser / text generator ABI ---------------------------------------------- */
+extern "C" int dsm_parse_traces_device(dsm_ctx *c, const char *d_text, const uint64_t *d_offsets,
+                                       uint64_t n_files, uint32_t cap, uint16_t *d_traces,
+                                       uint32_t *d_counts, int32_t *d_status, void *stream) {
+    if (!c || cap > c->cfg.max_instr) return DSM_E_INVAL;
+    if (n_files && (!d_text || !d_offsets || !d_traces || !d_counts)) return DSM_E_INVAL;
+    if (n_files == 0) return DSM_OK;
+    HIPCK(hipSetDevice(c->device));
+    /* one resident round of workgroups: a grid-stride loop over files with a second, partial
+     * round of workgroups would leave most of the chip idle at the end */
+    int per_cu = 0;
+    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)parse_kernel, 64 * PW, 0));
+    if (per_cu < 1) per_cu = 1;
+    uint64_t blocks = (n_files + PW - 1) / PW;
+    const uint64_t lim = (uint64_t)c->cus * per_cu;
+    if (blocks > lim) blocks = lim;
+    hipLaunchKernelGGL(parse_kernel, dim3((unsigned)blocks), dim3(64 * PW), 0, (hipStream_t)stream,
+                       (const uint8_t *)d_text, d_offsets, n_files, cap, c->cfg.max_instr,
+                       c->cfg.np, d_traces, d_counts, d_status);
+    HIPCK(hipGetLastError());
+    return DSM_OK;
+}
+
+extern "C" int dsm_parse_traces(dsm_ctx *c, const char *text, const uint64_t *offsets,
+                                uint64_t n_files, uint32_t cap, uint16_t *traces,
+                                uint32_t *counts, int32_t *status) {
+    if (!c || (n_files && (!text || !offsets || !traces || !counts))) return DSM_E_INVAL;
+    if (n_files == 0) return DSM_OK;
+    const uint64_t bytes = offsets[n_files] - offsets[0];
+    for (uint64_t f = 0; f < n_files; ++f)
+        if (offsets[f + 1] < offsets[f]) return DSM_E_INVAL;
+    HIPCK(hipSetDevice(c->device));
+    const uint32_t stride = c->cfg.max_instr;
+    char *d_text = nullptr;
+    uint64_t *d_off = nullptr;
+    uint16_t *d_tr = nullptr;
+    uint32_t *d_cn = nullptr;
+    int32_t *d_st = nullptr;
+    uint64_t *h_off = (uint64_t *)malloc((n_files + 1) * sizeof(uint64_t));
+    int rc = h_off ? DSM_OK : DSM_E_NOMEM;
+    if (rc == DSM_OK) {
+        for (uint64_t f = 0; f <= n_files; ++f) h_off[f] = offsets[f] - offsets[0];
+        if (hipMalloc((void **)&d_text, bytes + 64) != hipSuccess ||
+            hipMalloc((void **)&d_off, (n_files + 1) * sizeof(uint64_t)) != hipSuccess ||
+            hipMalloc((void **)&d_tr, n_files * stride * sizeof(uint16_t)) != hipSuccess ||
+            hipMalloc((void **)&d_cn, n_files * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc((void **)&d_st, n_files * sizeof(int32_t)) != hipSuccess)
+            rc = DSM_E_NOMEM;
+    }
+    if (rc == DSM_OK &&
+        (hipMemcpyAsync(d_text, text + offsets[0], bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+         hipMemcpyAsync(d_off, h_off, (n_files + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream) != hipSuccess))
+        rc = DSM_E_DEVICE;
+    if (rc == DSM_OK) rc = dsm_parse_traces_device(c, d_text, d_off, n_files, cap, d_tr, d_cn, d_st, c->stream);
+    if (rc == DSM_OK &&
+        (hipMemcpyAsync(traces, d_tr, n_files * stride * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+         hipMemcpyAsync(counts, d_cn, n_files * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+         (status && hipMemcpyAsync(status, d_st, n_files * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
+         hipStreamSynchronize(c->stream) != hipSuccess))
+        rc = DSM_E_DEVICE;
+    (void)hipStreamSynchronize(c->stream);
+    void *ptrs[] = {d_text, d_off, d_tr, d_cn, d_st};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    free(h_off);
+    return rc;
+}
+
+extern "C" int dsm_generate_text_device(dsm_ctx *c, const dsm_gen *g, uint64_t first_sys,
+                                        uint64_t n_sys, char *d_text, uint64_t *d_offsets,
+                                        void *stream) {
+    if (!c || !g || !d_offsets || g->dist < 0 || g->dist > 2 || g->n_instr > DSM_MAX_INSTR) return DSM_E_INVAL;
+    HIPCK(hipSetDevice(c->device));
+    const uint64_t n = n_sys * (uint64_t)c->cfg.np;
+    hipStream_t st = (hipStream_t)stream;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > (uint64_t)c->cus * 8) blocks = (uint64_t)c->cus * 8;
+    if (blocks == 0) blocks = 1;
+    if (c->cfg.np == 4)
+        hipLaunchKernelGGL(textlen_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, st, g->seed, g->dist, first_sys, n, g->n_instr, d_offsets);
+    else
+        hipLaunchKernelGGL(textlen_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, st, g->seed, g->dist, first_sys, n, g->n_instr, d_offsets);
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, d_offsets, n);
+    HIPCK(hipGetLastError());
+    if (!d_text) return DSM_OK;
+    uint64_t wblocks = (n + 3) / 4;
+    if (wblocks > (uint64_t)c->cus * 16) wblocks = (uint64_t)c->cus * 16;
+    if (wblocks == 0) wblocks = 1;
+    if (c->cfg.np == 4)
+        hipLaunchKernelGGL(textgen_kernel<4>, dim3((unsigned)wblocks), dim3(256), 0, st, g->seed, g->dist, first_sys, n, g->n_instr, (const uint64_t *)d_offsets, (uint8_t *)d_text);
+    else
+        hipLaunchKernelGGL(textgen_kernel<8>, dim3((unsigned)wblocks), dim3(256), 0, st, g->seed, g->dist, first_sys, n, g->n_instr, (const uint64_t *)d_offsets, (uint8_t *)d_text);
+    HIPCK(hipGetLastError());
+    return DSM_OK;
 }

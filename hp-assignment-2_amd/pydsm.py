@@ -98,6 +98,9 @@ def lib():
             "dsm_format_dumps_device": (i32, [vp, vp, u32, u64, vp, vp, vp]),
             "dsm_format_run_dumps_device": (i32, [vp, i32, u64, u64, vp, vp, vp]),
             "dsm_write_run_dumps": (i32, [vp, u64, u32, ctypes.c_char_p]),
+            "dsm_parse_traces_device": (i32, [vp, vp, vp, u64, u32, vp, vp, vp, vp]),
+            "dsm_parse_traces": (i32, [vp, vp, vp, u64, u32, vp, vp, vp]),
+            "dsm_generate_text_device": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -210,6 +213,37 @@ class Engine:
         f = np.zeros(64, dtype=np.uint8)
         _check(lib().dsm_get_node_state(self.ctx, sys, node, _ptr(d), _ptr(f)), "dsm_get_node_state")
         return d, f
+
+    # -- initializeProcessor's reader on the GPU ---------------------------------------------
+    def parse_traces(self, files, cap):
+        """files: list of bytes (core file contents, file f = node f % np of system f // np)
+        -> traces [n_sys, np, max_instr] u16, counts [n_sys, np] u32, status [n_sys, np] i32"""
+        n = len(files)
+        assert n % self.np == 0
+        text = np.frombuffer(b"".join(files) + b"\0" * 16, dtype=np.uint8)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(f) for f in files])
+        tr = np.zeros((n // self.np, self.np, self.max_instr), dtype=np.uint16)
+        cn = np.zeros((n // self.np, self.np), dtype=np.uint32)
+        st = np.zeros((n // self.np, self.np), dtype=np.int32)
+        _check(lib().dsm_parse_traces(self.ctx, _ptr(text), _ptr(off), n, cap, _ptr(tr), _ptr(cn),
+                                      _ptr(st)), "dsm_parse_traces")
+        return tr, cn, st
+
+    def parse_traces_device(self, d_text, d_offsets, n_files, cap, d_traces, d_counts, d_status,
+                            stream=0):
+        _check(lib().dsm_parse_traces_device(self.ctx, ctypes.c_void_p(d_text),
+                                             ctypes.c_void_p(d_offsets), n_files, cap,
+                                             ctypes.c_void_p(d_traces), ctypes.c_void_p(d_counts),
+                                             ctypes.c_void_p(d_status), ctypes.c_void_p(stream)),
+               "dsm_parse_traces_device")
+
+    def generate_text_device(self, dist, seed, n_instr, first_sys, n_sys, d_text, d_offsets,
+                             stream=0):
+        g = Gen(seed, DIST.get(dist, dist), n_instr)
+        _check(lib().dsm_generate_text_device(self.ctx, ctypes.byref(g), first_sys, n_sys,
+                                              ctypes.c_void_p(d_text), ctypes.c_void_p(d_offsets),
+                                              ctypes.c_void_p(stream)), "dsm_generate_text_device")
 
     # -- printProcessorState on the GPU ------------------------------------------------------
     def format_dumps_device(self, d_states, n_states, d_text, d_len, state_stride=1, stream=0):

@@ -6,6 +6,8 @@
  * internal C functions.  Each entry point below names the reference interface it replaces:
  *
  *   dsm_parse_trace_file / dsm_load_test_dir  <- initializeProcessor   assignment.c:776-822
+ *   dsm_parse_traces_device / dsm_parse_traces <- initializeProcessor's reader (:802-818) on
+ *                                                the GPU, for whole ensembles of core files
  *   dsm_format_dump / dsm_write_dump          <- printProcessorState   assignment.c:824-876
  *   dsm_format_dumps_device / dsm_format_run_dumps_device / dsm_write_run_dumps
  *                                             <- printProcessorState, on the GPU, for whole
@@ -201,6 +203,27 @@ int dsm_get_node_state(dsm_ctx *ctx, uint64_t sys, int node, dsm_node_state *dum
  * recorded on the run's own stream right before and after the kernel launch.  Waits for
  * the stop event. */
 int dsm_last_kernel_ms(dsm_ctx *ctx, float *ms);
+
+/* ---- initializeProcessor's trace reader on the GPU (:802-818) ---------------------- *
+ * n_files core files concatenated in d_text; file f is d_text[d_offsets[f] .. d_offsets[f+1])
+ * (d_offsets has n_files + 1 entries) and is node f % np of system f / np.  Each file is
+ * read as the reference reads it -- fgets(line, 20) chunks, each one instruction, scanned
+ * with "RD %hhx" / "WR %hhx %hhu" -- into d_traces[f * max_instr ..] (packed u16),
+ * d_counts[f] = instructions (at most cap <= max_instr) and d_status[f] (may be NULL) = 0 or
+ * the error at the first failing chunk, which also ends the count there: DSM_E_FORMAT (not
+ * RD/WR, or a conversion failed) or DSM_E_RANGE (home node >= np).  Asynchronous. */
+int dsm_parse_traces_device(dsm_ctx *ctx, const char *d_text, const uint64_t *d_offsets,
+                            uint64_t n_files, uint32_t cap, uint16_t *d_traces,
+                            uint32_t *d_counts, int32_t *d_status, void *stream);
+/* the same from host buffers (offsets[f] index into text); traces [n_files][max_instr] */
+int dsm_parse_traces(dsm_ctx *ctx, const char *text, const uint64_t *offsets, uint64_t n_files,
+                     uint32_t cap, uint16_t *traces, uint32_t *counts, int32_t *status);
+/* Synthetic core files in the shipped tests' format ("RD 0x%02x\n", "WR 0x%02x %u\n") for
+ * the generator's instructions of systems first_sys .. first_sys+n_sys-1.  Always writes
+ * d_offsets (n_sys*np + 1 entries; the last one is the total size); writes the text too
+ * unless d_text is NULL (size query). */
+int dsm_generate_text_device(dsm_ctx *ctx, const dsm_gen *gen, uint64_t first_sys, uint64_t n_sys,
+                             char *d_text, uint64_t *d_offsets, void *stream);
 
 /* ---- printProcessorState on the GPU (:824-876) ------------------------------------- *
  * Text of record k goes to d_text + k * DSM_DUMP_SLOT (16-byte aligned buffer), its length

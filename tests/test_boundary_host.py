@@ -148,7 +148,7 @@ def test_cli_without_gpu_fails_loudly(tmp_path):
     r = subprocess.run([pydsm.CLI_PATH, "sample"], cwd=tmp_path, capture_output=True, text=True)
     assert r.returncode == 1
     assert "dsm_open" in r.stderr
-    assert r.stdout.splitlines() == [f"Processor {n} initialized" for n in range(4)]
+    assert r.stdout == ""        # the core files are scanned on the GPU: nothing initialised
     assert not list(tmp_path.glob("core_*_output.txt"))
 
 

@@ -127,3 +127,126 @@ def test_gpu_format_full_size_final_view(dsm, torch):
         assert bytes(txt[i, :lens[k]]) == dsm.format_dump(int(k) % 8, recs[i]).encode(), k
         assert lens[k] == dsm.DUMP_BASE + int((recs[i][56:60] == 1).sum())
     del d_txt
+
+
+# ---- initializeProcessor's reader on the GPU (parse_kernel) --------------------------------
+def _host_expect(dsm, tmp_path, files, np_, cap):
+    """Expected (count, status, traces) per file from the host reader dsm_parse_trace_file
+    (glibc fgets + sscanf, the reference's :802-818 recipe) plus the home < np check."""
+    import ctypes
+    out = []
+    p = tmp_path / "core.txt"
+    for data in files:
+        p.write_bytes(data)
+        buf = np.zeros(max(cap, 1), dtype=np.uint16)
+        n = ctypes.c_uint32(0)
+        rc = dsm.lib().dsm_parse_trace_file(str(p).encode(), ctypes.c_void_p(buf.ctypes.data), cap,
+                                            ctypes.byref(n))
+        n = n.value
+        bad = np.nonzero(((buf[:n] >> 12) & 7) >= np_)[0]
+        if bad.size:
+            n, rc = int(bad[0]), dsm.E_RANGE
+        out.append((n, rc, buf[:n].copy()))
+    return out
+
+
+LINES = [b"RD 0x00\n", b"RD 0x1f\n", b"WR 0x02 100\n", b"WR 0x3f 255\n", b"WR 0x10 300\n",
+         b"RD 0x7f\n", b"WR 0x45 -1\n", b"RD 1F\n", b"RD\t0X2a\n", b"WR 0x11   +7\n",
+         b"RD 0x01\r\n", b"WR 0x00 0\n", b"RD 0x0\n", b"RD 0x\n", b"WR 0x2 08\n",
+         b"RD 0x11          RD 0x05\n",              # long line: second chunk is its own RD
+         b"WR 0x12 1                 \n",            # long line: the tail chunk is FORMAT
+         b"RD 0x13" + b" " * 12 + b"\n",             # 19 chars + '\n': the '\n' alone is a chunk
+         b"\n", b"XX 0x1\n", b"RD zz\n", b"WR 0x05\n", b"RD 0x80\n"]
+
+
+def _fuzz_files(rng, n_files, max_lines, bad_rate):
+    good = LINES[:15]
+    files = []
+    for _ in range(n_files):
+        k = int(rng.integers(0, max_lines + 1))
+        pick = [good[i] for i in rng.integers(0, len(good), k)]
+        if k and rng.random() < bad_rate:
+            pick[int(rng.integers(0, k))] = LINES[int(rng.integers(15, len(LINES)))]
+        data = b"".join(pick)
+        if data and rng.random() < 0.2:
+            data = data[:-1]                         # no trailing newline
+        files.append(data)
+    return files
+
+
+@pytest.mark.parametrize("np_,cap", [(4, 32), (8, 32), (8, 4096)])
+def test_gpu_parse_fuzzed_files_equal_host_reader(dsm, tmp_path, np_, cap):
+    rng = np.random.default_rng(cap + np_)
+    files = _fuzz_files(rng, 64 * np_, 60 if cap == 32 else 300, 0.3)
+    exp = _host_expect(dsm, tmp_path, files, np_, cap)
+    with dsm.Engine(np_, cap) as eng:
+        tr, cn, st = eng.parse_traces(files, cap)
+    tr, cn, st = tr.reshape(len(files), -1), cn.reshape(-1), st.reshape(-1)
+    for f, (n, rc, t) in enumerate(exp):
+        assert (int(cn[f]), int(st[f])) == (n, rc), (f, files[f][:200])
+        assert np.array_equal(tr[f, :n], t), f
+
+
+def test_gpu_parse_shipped_tests_and_cli_inputs(dsm):
+    import pyoracle as orc
+    files, exp = [], []
+    for test in TESTS:
+        for core in range(4):
+            files.append(open(os.path.join(inputs_dir(test), f"core_{core}.txt"), "rb").read())
+        exp.append(orc.load_test(inputs_dir(test)))
+    with dsm.Engine(4, 32) as eng:
+        tr, cn, st = eng.parse_traces(files, 32)
+    assert not st.any()
+    for i, (etr, ecn) in enumerate(exp):
+        assert np.array_equal(cn[i], ecn[0])
+        for core in range(4):
+            assert np.array_equal(tr[i, core, :cn[i, core]], etr[0, core, :ecn[0, core]])
+
+
+def test_gpu_parse_window_edges(dsm, tmp_path):
+    """files whose lines straddle the 1 KB window and 16-byte lane boundaries, long runs of
+    blank-free text, offsets that are not 16-byte aligned, and empty files."""
+    files = []
+    for pad in range(0, 40):
+        body = b"".join(LINES[i % 15] for i in range(pad, pad + 400))
+        files.append(b"RD 0x01" + b" " * (pad % 12) + b"\n" + body)
+    files += [b"", b"RD 0x01", b"WR 0x10 5"]
+    while len(files) % 4:
+        files.append(b"")
+    exp = _host_expect(dsm, tmp_path, files, 4, 512)
+    with dsm.Engine(4, 512) as eng:
+        tr, cn, st = eng.parse_traces(files, 512)
+    tr, cn, st = tr.reshape(len(files), -1), cn.reshape(-1), st.reshape(-1)
+    for f, (n, rc, t) in enumerate(exp):
+        assert (int(cn[f]), int(st[f])) == (n, rc), f
+        assert np.array_equal(tr[f, :n], t), f
+
+
+@pytest.mark.parametrize("dist", ["uniform", "hot", "evict"])
+def test_gpu_text_generator_round_trip(dsm, torch, dist):
+    """synthetic text files (generator -> text on the GPU) parse back to exactly the packed
+    traces of gen_kernel; a sample of files is also checked with the host reader."""
+    n_sys, n_instr = 2048, 4096
+    st = torch.cuda.current_stream().cuda_stream
+    with dsm.Engine(8, n_instr) as eng:
+        off = torch.zeros(n_sys * 8 + 1, dtype=torch.int64, device="cuda")
+        eng.generate_text_device(dist, 1, n_instr, 5000, n_sys, 0, off.data_ptr(), st)
+        torch.cuda.synchronize()
+        total = int(off[-1].item())
+        txt = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+        eng.generate_text_device(dist, 1, n_instr, 5000, n_sys, txt.data_ptr(), off.data_ptr(), st)
+        tr = torch.zeros((n_sys, 8, n_instr), dtype=torch.int16, device="cuda")
+        cn = torch.zeros((n_sys, 8), dtype=torch.int32, device="cuda")
+        ss = torch.full((n_sys, 8), 99, dtype=torch.int32, device="cuda")
+        eng.parse_traces_device(txt.data_ptr(), off.data_ptr(), n_sys * 8, n_instr, tr.data_ptr(),
+                                cn.data_ptr(), ss.data_ptr(), st)
+        gtr = torch.zeros_like(tr)
+        gcn = torch.zeros_like(cn)
+        eng.generate_device(dist, 1, n_instr, 5000, n_sys, gtr.data_ptr(), gcn.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert int(ss.abs().sum().item()) == 0
+        assert torch.equal(cn, gcn) and torch.equal(tr, gtr)
+        o = off.cpu().numpy()
+        t = txt.cpu().numpy()
+        files = [bytes(t[o[f]:o[f + 1]]) for f in (0, 1, 777, n_sys * 8 - 1)]
+        assert all(fl.startswith((b"RD 0x", b"WR 0x")) and fl.endswith(b"\n") for fl in files)
