@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(NT) fmt_kernel(const uint8_t *recs, uint64_t r
 
 
 /* ---- trace parser ------------------------------------------------------------------- */
-constexpr uint32_t PWIN = 1024, PHALO = 32, PW = 4;   /* window bytes, halo, waves/group */
+constexpr uint32_t PHALO = 32, PW = 4;   /* halo bytes (a chunk is <= 19), waves/group */
 
 /* aligned 16-byte load through the global address space (in-order vmcnt, not flat) */
 DEVI uint4 ldg16(const uint8_t *p) {
@@ -191,38 +191,40 @@ DEVI uint32_t hexval(uint32_t c) {            /* 0..15, or >= 16 */
  * those two shapes sscanf's result is exactly the one computed here (dsm_parse.h).
  * Returns 1 and *pk when the chunk has one of the shapes (and lim admits it). */
 DEVI uint32_t parse_fast(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t lim, uint32_t *pk) {
-    const uint32_t h1 = hexval((c1 >> 8) & 0xFFu), h2 = hexval((c1 >> 16) & 0xFFu);
+    /* branch-free: every condition is a bit, every choice a select */
+    const uint32_t b4 = c1 & 0xFFu, b5 = (c1 >> 8) & 0xFFu, b6 = (c1 >> 16) & 0xFFu, b7 = c1 >> 24;
+    const uint32_t h1 = hexval(b5), h2 = hexval(b6);
     const uint32_t a = (h1 << 4) | h2;
-    const bool hexok = (c1 & 0xFFu) == 'x' && h1 < 16u && h2 < 16u && a <= 0x7Fu;  /* else slow */
-    if (c0 == 0x30204452u && hexok && (c1 >> 24) == '\n' && lim >= 8u) {        /* "RD 0x" */
-        *pk = a << 8;
-        return 1u;
-    }
-    if (c0 == 0x30205257u && hexok && (c1 >> 24) == ' ') {                        /* "WR 0x" */
-        const uint32_t b8 = c2 & 0xFFu, b9 = (c2 >> 8) & 0xFFu, b10 = (c2 >> 16) & 0xFFu,
-                       b11 = c2 >> 24;
-        uint32_t v, n;
-        if (!is_dec(b8)) return 0u;
-        if (b9 == '\n') { v = b8 - '0'; n = 10u; }
-        else if (is_dec(b9) && b10 == '\n') { v = (b8 - '0') * 10u + (b9 - '0'); n = 11u; }
-        else if (is_dec(b9) && is_dec(b10) && b11 == '\n') {
-            v = (b8 - '0') * 100u + (b9 - '0') * 10u + (b10 - '0'); n = 12u;
-        } else return 0u;
-        if (lim < n) return 0u;
-        *pk = (1u << 15) | (a << 8) | (v & 0xFFu);
-        return 1u;
-    }
-    return 0u;
+    const uint32_t hexok = (uint32_t)(b4 == 'x') & (uint32_t)((h1 | h2) < 16u) & (uint32_t)(a <= 0x7Fu);
+    const uint32_t rd_ok = (uint32_t)(c0 == 0x30204452u) & hexok & (uint32_t)(b7 == '\n') & (uint32_t)(lim >= 8u);
+    const uint32_t b9 = (c2 >> 8) & 0xFFu, b10 = (c2 >> 16) & 0xFFu, b11 = c2 >> 24;
+    const uint32_t d8 = (c2 & 0xFFu) - '0', d9 = b9 - '0', d10 = b10 - '0';
+    const uint32_t e8 = d8 < 10u, e9 = d9 < 10u, e10 = d10 < 10u;
+    const uint32_t n10 = e8 & (uint32_t)(b9 == '\n');
+    const uint32_t n11 = e8 & e9 & (uint32_t)(b10 == '\n');
+    const uint32_t n12 = e8 & e9 & e10 & (uint32_t)(b11 == '\n');
+    const uint32_t v = n10 ? d8 : (n11 ? d8 * 10u + d9 : d8 * 100u + d9 * 10u + d10);
+    const uint32_t n = n10 ? 10u : (n11 ? 11u : 12u);
+    const uint32_t wr_ok = (uint32_t)(c0 == 0x30205257u) & hexok & (uint32_t)(b7 == ' ') &
+                           (n10 | n11 | n12) & (uint32_t)(lim >= n);
+    *pk = rd_ok ? (a << 8) : ((1u << 15) | (a << 8) | (v & 0xFFu));
+    return rd_ok | wr_ok;
 }
 
-/* One file per wave; windows double-buffered in registers (the next window's loads are in
- * flight while this one is scanned), staged in LDS for the chunk reads. */
+/* low n bits (n <= 32) */
+DEVI uint32_t lowmask(uint32_t n) { return n >= 32u ? 0xFFFFFFFFu : (1u << n) - 1u; }
+
+/* One file per wave; windows of 64 x BPL bytes, double-buffered in registers (the next
+ * window's loads are in flight while this one is scanned), staged in LDS for the chunk
+ * reads. */
+template <uint32_t BPL>
 __global__ void __launch_bounds__(64 * PW) parse_kernel(const uint8_t *text, const uint64_t *off,
                                                       uint64_t n_files, uint32_t cap,
                                                       uint32_t stride, int np, uint16_t *traces,
                                                       uint32_t *counts, int32_t *status) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_txt[PW][PWIN + PHALO + 16];
-    __shared__ uint16_t s_list[PW][PWIN];               /* chunk offsets of the window */
+    constexpr uint32_t K = BPL / 16, WIN = 64 * BPL;
+    __shared__ __attribute__((aligned(16))) uint8_t s_txt[PW][WIN + PHALO + 16];
+    __shared__ uint16_t s_list[PW][WIN];                /* chunk offsets of the window */
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint8_t *const st = s_txt[wv];
     uint16_t *const sl = s_list[wv];
@@ -233,51 +235,63 @@ __global__ void __launch_bounds__(64 * PW) parse_kernel(const uint8_t *text, con
         const uint64_t last = b1 > wbeg ? ((b1 - 1) & ~15ull) : wbeg;     /* last in-file block */
         /* window loads: always issued (address clamped into the file) so they land straight
          * in their registers; bytes outside the file are masked by position */
-        auto load = [&](uint64_t wa, uint4 &v, uint4 &h) {
-            const uint64_t q = wa + 16u * lane, hq = wa + PWIN + 16u * (lane & 1u);
-            v = ldg16(text + (q < last ? q : last));
+        auto load = [&](uint64_t wa, uint4 (&v)[K], uint4 &h) {
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) {
+                const uint64_t q = wa + BPL * lane + 16u * k;
+                v[k] = ldg16(text + (q < last ? q : last));
+            }
+            const uint64_t hq = wa + WIN + 16u * (lane & 1u);
             h = ldg16(text + (hq < last ? hq : last));
         };
-        uint32_t ls_rel = 0;          /* start of the line open at the window start, - b0   */
+        /* positions below are 32-bit, relative to wbeg (files are < 4 GiB) */
+        const uint32_t s0 = (uint32_t)(b0 - wbeg), e0 = (uint32_t)(b1 - wbeg);   /* file [s0, e0) */
+        uint32_t ls_rel = s0;         /* start of the line open at the window start          */
         uint32_t idx0 = 0;            /* chunks before the window                           */
         uint32_t err = 0xFFFFFFFFu;   /* first failing chunk: index * 8 + error class        */
-        uint4 va, ha, vb, hb;
+        uint4 va[K], vb[K], ha, hb;
         uint64_t wa = wbeg;
         bool more = wbeg < b1;
         if (more) load(wa, va, ha);
-        auto window = [&](uint64_t wa, const uint4 &v, const uint4 &h) {
-            /* (1) stage [wa, wa + PWIN + PHALO) */
+        auto window = [&](uint64_t wa, const uint4 (&v)[K], const uint4 &h) {
+            /* (1) stage [wa, wa + WIN + PHALO) */
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            reinterpret_cast<uint4 *>(st)[lane] = v;
-            if (lane < 2) reinterpret_cast<uint4 *>(st + PWIN)[lane] = h;
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) reinterpret_cast<uint4 *>(st)[K * lane + k] = v[k];
+            if (lane < 2) reinterpret_cast<uint4 *>(st + WIN)[lane] = h;
             /* (2) newlines among this lane's in-file bytes */
-            const uint64_t base = wa + 16u * lane;
-            const uint32_t lo = base < b0 ? (uint32_t)(b0 - base) : 0u;          /* < 16 */
-            const uint32_t hi = base + 16 <= b1 ? 16u : (base < b1 ? (uint32_t)(b1 - base) : 0u);
-            const uint32_t fm = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t wr0 = (uint32_t)(wa - wbeg);
+            const uint32_t base = wr0 + BPL * lane;
+            const uint32_t lo = base < s0 ? s0 - base : 0u;                      /* < 16 */
+            const uint32_t hi = base + BPL <= e0 ? BPL : (base < e0 ? e0 - base : 0u);
+            const uint32_t fm = hi > lo ? (lowmask(hi) & ~lowmask(lo)) : 0u;
             uint32_t nl = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {                /* bytes == '\n', 4 at a time */
-                const uint32_t t = w[k] ^ 0x0A0A0A0Au;
+            for (uint32_t k = 0; k < 4 * K; ++k) {       /* bytes == '\n', 4 at a time */
+                const uint4 &q = v[k >> 2];
+                const uint32_t wd = (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
+                const uint32_t t = wd ^ 0x0A0A0A0Au;
                 const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
                 nl |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
             }
             nl &= fm;
             /* (3) line start at this lane's first byte: max over lower lanes of (last nl + 1) */
-            const uint32_t my = nl ? (uint32_t)(base + (31u - __builtin_clz(nl)) + 1u - b0) : 0u;
+            const uint32_t my = nl ? base + (31u - __builtin_clz(nl)) + 1u : 0u;
             const uint32_t incl = wave_incl_max(my);
             const uint32_t lsr = umax(DPP(incl, 0x138, 0xF, 0xF, true), ls_rel);  /* wave_shr:1 */
             /* (4) chunk starts: line starts, and every 19 bytes into a longer line */
-            const uint32_t din = lo > 0 ? 0u : (uint32_t)(base - b0) - lsr;   /* distance at byte 0 */
-            const uint32_t fnl = nl ? __builtin_ctz(nl) : 15u;
-            uint32_t cs;
-            if (lo > 0 || din + (fnl < 15u ? fnl : 15u) < DP_CHUNK) {
-                cs = (((nl << 1) & 0xFFFFu) | (lo > 0 ? (1u << lo) : (din == 0 ? 1u : 0u))) & fm;
-            } else {                                     /* a line of >= 19 bytes reaches here */
+            const uint32_t din = lo > 0 ? 0u : base - lsr;       /* distance from line start */
+            const uint32_t fnl = nl ? __builtin_ctz(nl) : BPL - 1u;
+            uint32_t cs = ((nl << 1) | (lo > 0 ? (1u << lo) : (din == 0 ? 1u : 0u))) & fm;
+            /* a byte at distance >= 19 from its line start: either in the line open at the
+             * lane start (din), or after a run of 19 non-newline bytes inside the lane */
+            const uint32_t r = ~nl & fm;
+            const uint32_t t1 = r & (r >> 1), t2 = t1 & (t1 >> 2), t4 = t2 & (t2 >> 4), t8 = t4 & (t4 >> 8);
+            const bool run19 = BPL > DP_CHUNK && (t8 & (t1 >> 16) & (r >> 18)) != 0u;
+            if ((lo == 0 && din + (fnl < BPL - 1u ? fnl : BPL - 1u) >= DP_CHUNK) || run19) {   /* long line */
                 uint32_t d = din % DP_CHUNK;
                 cs = 0;
-                for (int j = 0; j < 16; ++j) {
+                for (uint32_t j = 0; j < BPL; ++j) {
                     const uint32_t in = (fm >> j) & 1u;
                     cs |= (uint32_t)(in && d == 0) << j;
                     d = ((nl >> j) & 1u) ? 0u : (d == DP_CHUNK - 1 ? 0u : d + in);
@@ -289,23 +303,22 @@ __global__ void __launch_bounds__(64 * PW) parse_kernel(const uint8_t *text, con
             const uint32_t T = __builtin_amdgcn_readlane(isum, 63);
             {
                 uint32_t k = isum - nc;
-                for (uint32_t m = cs; m; m &= m - 1u) sl[k++] = (uint16_t)(16u * lane + __builtin_ctz(m));
+                for (uint32_t m = cs; m; m &= m - 1u) sl[k++] = (uint16_t)(BPL * lane + __builtin_ctz(m));
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             /* (6) one chunk per lane per round: parse from LDS, coalesced 2-byte stores */
             const uint32_t tmax = cap - idx0 < T ? cap - idx0 : T;
+            const uint32_t rem = e0 - wr0;                       /* file bytes from wa on */
             for (uint32_t t0 = 0; t0 < tmax; t0 += 64) {
                 const uint32_t t = t0 + lane;
                 if (t < tmax) {
                     const uint32_t o = sl[t];
-                    const uint64_t p = wa + o;
-                    const uint32_t lim = (b1 - p) < DP_CHUNK ? (uint32_t)(b1 - p) : DP_CHUNK;
+                    const uint32_t lim = rem - o < DP_CHUNK ? rem - o : DP_CHUNK;
                     const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
-                    const uint32_t sh = (o & 3u) * 8u;
                     const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
-                    const uint32_t c0 = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;
-                    const uint32_t c1 = sh ? (d1 >> sh) | (d2 << (32 - sh)) : d1;
-                    const uint32_t c2 = sh ? (d2 >> sh) | (d3 << (32 - sh)) : d2;
+                    const uint32_t c0 = __builtin_amdgcn_alignbyte(d1, d0, o & 3u);
+                    const uint32_t c1 = __builtin_amdgcn_alignbyte(d2, d1, o & 3u);
+                    const uint32_t c2 = __builtin_amdgcn_alignbyte(d3, d2, o & 3u);
                     uint32_t pk = 0;
                     int rc = 0;
                     if (!parse_fast(c0, c1, c2, lim, &pk)) {
@@ -328,13 +341,13 @@ __global__ void __launch_bounds__(64 * PW) parse_kernel(const uint8_t *text, con
         /* the next window's loads are unconditional (clamped): a conditional load makes the
          * waitcnt at the join assume it was not issued, i.e. wait for it right away */
         while (more) {
-            const uint64_t wn = wa + PWIN;
+            const uint64_t wn = wa + WIN;
             load(wn, vb, hb);
             window(wa, va, ha);
             more = wn < b1 && idx0 < cap && err == 0xFFFFFFFFu;
             if (!more) break;
             wa = wn;
-            const uint64_t wn2 = wa + PWIN;
+            const uint64_t wn2 = wa + WIN;
             load(wn2, va, ha);
             window(wa, vb, hb);
             more = wn2 < b1 && idx0 < cap && err == 0xFFFFFFFFu;
@@ -554,17 +567,26 @@ extern "C" int dsm_parse_traces_device(dsm_ctx *c, const char *d_text, const uin
     if (n_files && (!d_text || !d_offsets || !d_traces || !d_counts)) return DSM_E_INVAL;
     if (n_files == 0) return DSM_OK;
     HIPCK(hipSetDevice(c->device));
+    /* DSM_PARSE_BPL=16|32: bytes per lane per window (1 or 2 KB windows), for A/B runs */
+    const char *e = getenv("DSM_PARSE_BPL");
+    const bool b32 = e ? atoi(e) == 32 : true;
+    const void *fn = b32 ? (const void *)parse_kernel<32> : (const void *)parse_kernel<16>;
     /* one resident round of workgroups: a grid-stride loop over files with a second, partial
      * round of workgroups would leave most of the chip idle at the end */
     int per_cu = 0;
-    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)parse_kernel, 64 * PW, 0));
+    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * PW, 0));
     if (per_cu < 1) per_cu = 1;
     uint64_t blocks = (n_files + PW - 1) / PW;
     const uint64_t lim = (uint64_t)c->cus * per_cu;
     if (blocks > lim) blocks = lim;
-    hipLaunchKernelGGL(parse_kernel, dim3((unsigned)blocks), dim3(64 * PW), 0, (hipStream_t)stream,
-                       (const uint8_t *)d_text, d_offsets, n_files, cap, c->cfg.max_instr,
-                       c->cfg.np, d_traces, d_counts, d_status);
+    if (b32)
+        hipLaunchKernelGGL(parse_kernel<32>, dim3((unsigned)blocks), dim3(64 * PW), 0, (hipStream_t)stream,
+                           (const uint8_t *)d_text, d_offsets, n_files, cap, c->cfg.max_instr,
+                           c->cfg.np, d_traces, d_counts, d_status);
+    else
+        hipLaunchKernelGGL(parse_kernel<16>, dim3((unsigned)blocks), dim3(64 * PW), 0, (hipStream_t)stream,
+                           (const uint8_t *)d_text, d_offsets, n_files, cap, c->cfg.max_instr,
+                           c->cfg.np, d_traces, d_counts, d_status);
     HIPCK(hipGetLastError());
     return DSM_OK;
 }

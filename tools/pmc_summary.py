@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""tools/pmc_summary.py <prof_dir> -- per-kernel averages of the rocprofv3 PMC passes and the
+"""tools/pmc_summary.py <prof_dir> [kernel-substring,...] -- per-kernel averages of the rocprofv3 PMC passes and the
 kernel-trace stats written by tools/profile.sh."""
 import collections
 import csv
@@ -8,6 +8,7 @@ import os
 import sys
 
 d = sys.argv[1]
+keep = sys.argv[2].split(",") if len(sys.argv) > 2 else ["sim_kernel", "gen_kernel"]
 print("== kernel stats (", d, ")")
 for f in glob.glob(os.path.join(d, "kt", "*kernel_stats.csv")):
     for r in csv.DictReader(open(f)):
@@ -17,7 +18,7 @@ for f in glob.glob(os.path.join(d, "pmc_*", "*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in agg.items():
-    if "sim_kernel" not in k and "gen_kernel" not in k:
+    if not any(x in k for x in keep):
         continue
     print("==", k[:100])
     for c, v in sorted(cs.items()):
