@@ -77,6 +77,31 @@ def cpu_baseline(dist, n_instr, seed, n_sample, threads):
                             f" {dt:.2f} s wall, {threads} OpenMP threads, traces generated lazily)")
 
 
+def cpu_baseline_reference(dist, n_instr, seed, n_sample, procs):
+    """The REFERENCE's own transition code (assignment.c handler + issue text, compiled
+    gcc -O2 from /root/reference by oracle/build_ref.sh into oracle/_ref/, driven under the
+    same lock-step schedule) over systems 0..n_sample-1 of the same workload, in `procs`
+    forked processes.  Timed: run_system only (trace generation + initializeProcessor
+    excluded, as the GPU's timed region starts with traces in HBM); rate = transactions /
+    the slowest process's simulation time.  None when oracle/_ref was not built."""
+    exe = os.path.join(ORACLE, "_ref", f"ref_lockstep_np{NP}")
+    if not os.path.exists(exe):
+        return None
+    import subprocess
+    dcode = {"uniform": 0, "hot": 1, "evict": 2}[dist]
+    r = subprocess.run([exe, "bench", str(dcode), str(seed), str(n_instr), "0", str(n_sample),
+                        str(procs)], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return None
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    t = d["sim_ns_max"] * 1e-9
+    return dict(value=d["msgs"] / t, unit=UNIT, cores=procs, kind="reference",
+                sample=f"systems 0..{n_sample - 1} of the same workload ({d['msgs']} transactions); "
+                       f"assignment.c's own handler/issue code (gcc -O2) under the lock-step "
+                       f"schedule, {procs} processes, simulation time of the slowest "
+                       f"{t:.2f} s (generation and initializeProcessor untimed)")
+
+
 def traffic_from_profiles(config):
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -99,6 +124,7 @@ def main():
     ap.add_argument("--fused", action="store_true",
                     help="generate instructions inside the transition kernel (no HBM traces)")
     ap.add_argument("--cpu-sample", type=int, default=262144)
+    ap.add_argument("--cpu-ref-sample", type=int, default=65536)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dump", action="store_true", help="skip the GPU dump-formatter phase")
     ap.add_argument("--parse-systems", type=int, default=65536,
@@ -257,13 +283,17 @@ def main():
         ach = alg_bytes / (kavg * 1e-3) / 1e9
         roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
-                    kernel="sim_kernel<8,12,4,packed> (lock-step transition kernel)",
+                    kernel="sim_kernel<8, 12, 4, false, false, 5> (lock-step transition kernel; 4-wave groups, ring 12, packed traces)",
                     algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),
                     per_unit="2 B per consumed packed instruction + 32 B result + 4*np B counts per system")
-        tr = traffic_from_profiles(args.config)
-        if tr and not args.fused:
-            roof["traffic"] = tr.get("bytes_per_launch")
-            roof["traffic_source"] = tr.get("source")
+        tr = traffic_from_profiles(args.config) or {}
+        if tr.get("sim_kernel") and not args.fused:
+            roof["traffic"] = tr["sim_kernel"].get("bytes_per_launch")
+            roof["traffic_source"] = tr["sim_kernel"].get("source")
+        for phase, kname in ((trace_parse, "parse_kernel"), (dump_stream, "fmt_kernel"),
+                             (trace_stream, "gen_kernel")):
+            if phase is not None and tr.get(kname):
+                phase["traffic"] = tr[kname].get("bytes_per_launch")
         parity = None
         if args.config == "random" and rank == 0 and first == 0 and n_sys >= 4096:
             g = np.load(os.path.join(REPO, "tests", "golden", "ensemble", "np8_uniform.npy"))
@@ -272,10 +302,14 @@ def main():
                              r["msgs"].astype(np.uint64), r["instrs"].astype(np.uint64),
                              r["dump_hash"], r["final_hash"]], axis=1)
             parity = "golden[0:4096] bit-exact" if np.array_equal(mine, g) else "GOLDEN MISMATCH"
-        cpu = None
+        cpu = cpu_port = None
         if world == 1 and not args.no_cpu:
-            threads = min(16, os.cpu_count() or 1)
-            _, cpu = cpu_baseline(dname, n_instr, seed, min(args.cpu_sample, n_sys), threads)
+            threads = min(16, os.cpu_count() or 1)     # the GPU box's host share is 16 cores
+            cpu = cpu_baseline_reference(dname, n_instr, seed, min(args.cpu_ref_sample, n_sys),
+                                         threads)
+            _, cpu_port = cpu_baseline(dname, n_instr, seed, min(args.cpu_sample, n_sys), threads)
+            if cpu is None:
+                cpu, cpu_port = cpu_port, None
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": UNIT, "n_gpus": world,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed_max / K * 1e3, 3),
@@ -288,6 +322,7 @@ def main():
                                  "packed u16 traces resident in HBM"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "cpu_port": cpu_port,
             "trace_stream": trace_stream,
             "trace_parse": trace_parse,
             "dump_stream": dump_stream,

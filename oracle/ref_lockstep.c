@@ -22,6 +22,8 @@
  *                                            dumps written to CWD by printProcessorState)
  *   ref_lockstep gen <dist> <seed> <n_instr> <first_sys> <n_sys> <out.bin>
  *   ref_lockstep fmt <recs.bin> <out.bin>   (printProcessorState of 64-byte records)
+ *   ref_lockstep bench <dist> <seed> <n_instr> <first> <n> <nproc>
+ *                                            (CPU baseline: timed run_system, forked slices)
  * out.bin: per system one dsm_res, then NUM_PROCS dump records, then NUM_PROCS final records.
  */
 #include <stdio.h>
@@ -30,6 +32,8 @@
 #include <unistd.h>
 #include <ctype.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
+#include <time.h>
 #include <stdint.h>
 #include "dsm_common.h"
 
@@ -259,6 +263,83 @@ int main(int argc, char **argv) {
             char p[64]; snprintf(p, sizeof p, "tests/empty/core_%d.txt", t); unlink(p);
         }
         rmdir("tests/empty"); rmdir("tests"); if (chdir("/")) {} rmdir(tmpl);
+        return 0;
+    }
+    if (argc == 8 && !strcmp(argv[1], "bench")) {
+        /* CPU baseline: the reference's own handler text under the lock-step schedule over
+         * systems first .. first+n-1 of the generator, in nproc forked processes (one slice
+         * each).  Only run_system is timed (CLOCK_MONOTONIC around each call): trace
+         * generation and initializeProcessor's file reads stay outside, as the GPU's timed
+         * region starts with the traces resident in HBM.  Prints one JSON line. */
+        int dist = atoi(argv[2]);
+        uint64_t seed = strtoull(argv[3], 0, 0);
+        int n_instr = atoi(argv[4]);
+        uint64_t first = strtoull(argv[5], 0, 0), n = strtoull(argv[6], 0, 0);
+        int nproc = atoi(argv[7]);
+        if (n_instr > MAX_INSTR_NUM || nproc < 1 || nproc > 256) { fprintf(stderr, "bad args\n"); return 1; }
+        int fds[256][2];
+        for (int p = 0; p < nproc; ++p) {
+            if (pipe(fds[p])) { perror("pipe"); return 1; }
+            pid_t pid = fork();
+            if (pid < 0) { perror("fork"); return 1; }
+            if (pid == 0) {
+                close(fds[p][0]);
+                const uint64_t lo = first + n * (uint64_t)p / (uint64_t)nproc;
+                const uint64_t hi = first + n * (uint64_t)(p + 1) / (uint64_t)nproc;
+                char tmpl[] = "/tmp/refbenchXXXXXX";
+                if (!mkdtemp(tmpl) || chdir(tmpl)) _exit(1);
+                mkdir("tests", 0700); mkdir("tests/empty", 0700);
+                for (int t = 0; t < NUM_PROCS; ++t) {
+                    char q[64]; snprintf(q, sizeof q, "tests/empty/core_%d.txt", t);
+                    FILE *e = fopen(q, "w"); if (e) fclose(e);
+                }
+                if (!freopen("/dev/null", "w", stdout)) _exit(1);
+                uint64_t msgs = 0, instrs = 0, ns = 0;
+                for (uint64_t sy = lo; sy < hi; ++sy) {
+                    for (int t = 0; t < NUM_PROCS; ++t) {
+                        reset_ctx(t);
+                        initializeProcessor(t, &C[t].node, "empty");
+                        for (int i = 0; i < n_instr; ++i) {
+                            uint16_t w = dsm_gen_instr(seed, dist, NUM_PROCS, sy, t, (uint32_t)i);
+                            C[t].node.instructions[i].type = (w >> 15) ? 'W' : 'R';
+                            C[t].node.instructions[i].address = (byte)((w >> 8) & 0x7F);
+                            C[t].node.instructions[i].value = (byte)(w & 0xFF);
+                        }
+                        C[t].node.instructionCount = n_instr;
+                    }
+                    struct timespec a, b;
+                    clock_gettime(CLOCK_MONOTONIC, &a);
+                    run_system(&res, dump, fin);
+                    clock_gettime(CLOCK_MONOTONIC, &b);
+                    ns += (uint64_t)(b.tv_sec - a.tv_sec) * 1000000000ull + (uint64_t)(b.tv_nsec - a.tv_nsec);
+                    msgs += res.msgs;
+                    instrs += res.instrs;
+                }
+                for (int t = 0; t < NUM_PROCS; ++t) {
+                    char q[64]; snprintf(q, sizeof q, "tests/empty/core_%d.txt", t); unlink(q);
+                }
+                rmdir("tests/empty"); rmdir("tests"); if (chdir("/")) {} rmdir(tmpl);
+                uint64_t outv[3] = {msgs, instrs, ns};
+                if (write(fds[p][1], outv, sizeof outv) != (ssize_t)sizeof outv) _exit(1);
+                _exit(0);
+            }
+            close(fds[p][1]);
+        }
+        uint64_t msgs = 0, instrs = 0, ns_max = 0, ns_sum = 0;
+        int ok = 1;
+        for (int p = 0; p < nproc; ++p) {
+            uint64_t v[3];
+            if (read(fds[p][0], v, sizeof v) != (ssize_t)sizeof v) ok = 0;
+            else { msgs += v[0]; instrs += v[1]; ns_sum += v[2]; if (v[2] > ns_max) ns_max = v[2]; }
+            close(fds[p][0]);
+        }
+        int stt;
+        while (wait(&stt) > 0) {}
+        if (!ok) { fprintf(stderr, "bench: a worker failed\n"); return 1; }
+        printf("{\"msgs\": %llu, \"instrs\": %llu, \"systems\": %llu, \"nproc\": %d, "
+               "\"sim_ns_max\": %llu, \"sim_ns_sum\": %llu}\n",
+               (unsigned long long)msgs, (unsigned long long)instrs, (unsigned long long)n, nproc,
+               (unsigned long long)ns_max, (unsigned long long)ns_sum);
         return 0;
     }
     if (argc == 4 && !strcmp(argv[1], "fmt")) {
