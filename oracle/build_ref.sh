@@ -6,6 +6,7 @@
 #   oracle/_ref/cache_simulator_ref    assignment.c compiled unmodified (gcc -O2 -fopenmp)
 #   oracle/_ref/ref_lockstep_np4_i32   reference handler text under the lock-step schedule,
 #                                      NUM_PROCS=4, MAX_INSTR_NUM=32 (the shipped sizes)
+#   oracle/_ref/ref_lockstep_np4_i32_dbg  the same with DEBUG_INSTR (issue-order printf)
 #   oracle/_ref/ref_lockstep_np4       NUM_PROCS=4, MAX_INSTR_NUM=4096
 #   oracle/_ref/ref_lockstep_np8       NUM_PROCS=8, MAX_INSTR_NUM=4096
 set -euo pipefail
@@ -34,6 +35,8 @@ extract 824 876 frag_print.inc   '^void printProcessorState'
 
 CFLAGS="-O2 -w -I$TMP -I$HERE"
 gcc $CFLAGS -DNUM_PROCS=4 -DMAX_INSTR_NUM=32   "$HERE/ref_lockstep.c" -o "$OUT/ref_lockstep_np4_i32"
+# the reference's own DEBUG_INSTR printf (:595-598) kept: its issue order under the schedule
+gcc $CFLAGS -DNUM_PROCS=4 -DMAX_INSTR_NUM=32 -DDEBUG_INSTR "$HERE/ref_lockstep.c" -o "$OUT/ref_lockstep_np4_i32_dbg"
 gcc $CFLAGS -DNUM_PROCS=4 -DMAX_INSTR_NUM=4096 "$HERE/ref_lockstep.c" -o "$OUT/ref_lockstep_np4"
 gcc $CFLAGS -DNUM_PROCS=8 -DMAX_INSTR_NUM=4096 "$HERE/ref_lockstep.c" -o "$OUT/ref_lockstep_np8"
 gcc -O2 -fopenmp "$SRC" -o "$OUT/cache_simulator_ref"

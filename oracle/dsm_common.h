@@ -110,4 +110,18 @@ static inline uint16_t dsm_gen_instr(uint64_t seed, int dist, int np, uint64_t s
     return (uint16_t)((wr << 15) | (addr << 8) | val);
 }
 
+/* Seeded schedule exploration.  In each round every node whose schedule
+ * gives it an action (pop its inbox head / issue / dump, Appendix A) takes it only if
+ * dsm_sched_act() says so, otherwise it stalls for that round -- a legal interleaving of the
+ * reference's free-running threads.  thresh >= 0x10000 is the plain lock-step schedule.  A
+ * round counts (and the system continues) while any node HAS an action, taken or not. */
+#define DSM_SCHED_LOCKSTEP 0x10000u
+static inline int dsm_sched_act(uint64_t seed, uint32_t thresh, uint64_t sys, uint32_t round,
+                                int node) {
+    if (thresh >= DSM_SCHED_LOCKSTEP) return 1;
+    const uint64_t key = (sys << 26) ^ ((uint64_t)round << 3) ^ (uint64_t)node;
+    const uint32_t h = (uint32_t)(dsm_splitmix(seed * 0x9E3779B97F4A7C15ULL + key) >> 48);
+    return h < thresh;
+}
+
 #endif

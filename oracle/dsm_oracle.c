@@ -308,9 +308,14 @@ static inline uint16_t fetch(const tsrc *t, int np, int node, uint32_t i) {
     return t->trace[(size_t)node * t->stride + i];
 }
 
+typedef struct {
+    uint64_t seed; uint32_t thresh; uint64_t sys;      /* schedule (dsm_sched_act)         */
+    uint32_t *ev; uint32_t ev_cap; uint32_t ev_n;       /* issue order: node << 16 | instr   */
+} oextra;
+
 static int run_one(int np, const tsrc *t, const uint32_t *counts, uint32_t ring_cap,
                    dsm_res *res, dsm_rec *dump_out, dsm_rec *fin_out, uint64_t *by_type,
-                   omsg *ring_mem) {
+                   omsg *ring_mem, oextra *x) {
     osys y;
     dsm_rec dump[8];
     memset(&y, 0, sizeof y);
@@ -329,6 +334,14 @@ static int run_one(int np, const tsrc *t, const uint32_t *counts, uint32_t ring_
         y.nst = 0;
         for (int me = 0; me < np; ++me) {
             onode *nd = &y.n[me];
+            if (x && x->thresh < DSM_SCHED_LOCKSTEP) {          /* exploration: may stall */
+                const int avail = nd->count > 0 ||
+                    (!WAITING(nd) && (nd->s.issued < counts[me] || !(nd->s.flags & 2)));
+                if (avail && !dsm_sched_act(x->seed, x->thresh, x->sys, r, me)) {
+                    acted = 1;
+                    continue;
+                }
+            }
             if (nd->count > 0) {                                     /* drain :158-169 */
                 omsg m = nd->ring[nd->head];
                 nd->head = (uint16_t)((nd->head + 1) % DSM_REF_RING_CAP);
@@ -338,6 +351,10 @@ static int run_one(int np, const tsrc *t, const uint32_t *counts, uint32_t ring_
             } else if (WAITING(nd)) {                                /* :578-581 */
             } else if (nd->s.issued < counts[me]) {                  /* :590-592 */
                 uint16_t ins = fetch(t, np, me, nd->s.issued);
+                if (x && x->ev) {                              /* DEBUG_INSTR order :596-597 */
+                    if (x->ev_n < x->ev_cap) x->ev[x->ev_n] = ((uint32_t)me << 16) | ins;
+                    x->ev_n++;
+                }
                 nd->s.issued++;
                 issue(&y, me, ins);
                 acted = 1; instrs++;
@@ -386,7 +403,7 @@ int orc_run_system(int np, const uint16_t *trace, const uint32_t *counts, uint32
     static __thread omsg *ring_mem;
     if (!ring_mem) ring_mem = (omsg *)malloc(sizeof(omsg) * 8 * DSM_REF_RING_CAP);
     tsrc t; memset(&t, 0, sizeof t); t.trace = trace; t.stride = stride;
-    return run_one(np, &t, counts, ring_cap, res, dump, fin, by_type, ring_mem);
+    return run_one(np, &t, counts, ring_cap, res, dump, fin, by_type, ring_mem, NULL);
 }
 
 int orc_run_packed(int np, const uint16_t *traces, const uint32_t *counts, uint32_t stride,
@@ -404,7 +421,7 @@ int orc_run_packed(int np, const uint16_t *traces, const uint32_t *counts, uint3
             t.trace = traces + (size_t)i * np * stride; t.stride = stride;
             err |= run_one(np, &t, counts + (size_t)i * np, ring_cap, &res[i],
                            dump ? dump + (size_t)i * np : NULL, fin ? fin + (size_t)i * np : NULL,
-                           tot, ring_mem);
+                           tot, ring_mem, NULL);
         }
         free(ring_mem);
     }
@@ -427,11 +444,39 @@ int orc_run_generated(int np, int dist, uint64_t seed, uint32_t n_instr, uint64_
         for (int64_t i = 0; i < (int64_t)n_sys; ++i) {
             tsrc t; memset(&t, 0, sizeof t);
             t.gen = 1; t.dist = dist; t.seed = seed; t.sys = first_sys + (uint64_t)i;
-            err |= run_one(np, &t, counts, ring_cap, &res[i], NULL, NULL, tot, ring_mem);
+            err |= run_one(np, &t, counts, ring_cap, &res[i], NULL, NULL, tot, ring_mem, NULL);
         }
         free(ring_mem);
     }
     if (by_type) for (int k = 0; k < DSM_NTYPES; ++k) by_type[k] += tot[k];
+    return err ? -1 : 0;
+}
+
+int orc_run_packed_ex(int np, const uint16_t *traces, const uint32_t *counts, uint32_t stride,
+                      uint64_t n_sys, uint32_t ring_cap, uint64_t sched_seed,
+                      uint32_t sched_thresh, uint64_t first_sys, dsm_res *res, dsm_rec *dump,
+                      dsm_rec *fin, uint32_t *issue, uint32_t issue_cap, uint32_t *issue_n,
+                      int nthreads) {
+    int err = 0;
+    (void)nthreads;
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1) reduction(|:err)
+    {
+        omsg *ring_mem = (omsg *)malloc(sizeof(omsg) * 8 * DSM_REF_RING_CAP);
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t i = 0; i < (int64_t)n_sys; ++i) {
+            tsrc t; memset(&t, 0, sizeof t);
+            t.trace = traces + (size_t)i * np * stride; t.stride = stride;
+            oextra x;
+            memset(&x, 0, sizeof x);
+            x.seed = sched_seed; x.thresh = sched_thresh; x.sys = first_sys + (uint64_t)i;
+            if (issue) { x.ev = issue + (size_t)i * issue_cap; x.ev_cap = issue_cap; }
+            err |= run_one(np, &t, counts + (size_t)i * np, ring_cap, &res[i],
+                           dump ? dump + (size_t)i * np : NULL, fin ? fin + (size_t)i * np : NULL,
+                           NULL, ring_mem, &x);
+            if (issue_n) issue_n[i] = x.ev_n;
+        }
+        free(ring_mem);
+    }
     return err ? -1 : 0;
 }
 

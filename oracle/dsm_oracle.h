@@ -33,6 +33,15 @@ int orc_run_generated(int np, int dist, uint64_t seed, uint32_t n_instr, uint64_
                       uint64_t n_sys, uint32_t ring_cap, dsm_res *res, uint64_t *by_type,
                       int nthreads);
 
+/* orc_run_packed plus seeded schedule exploration (dsm_sched_act with system id
+ * first_sys + i; sched_thresh >= DSM_SCHED_LOCKSTEP = lock-step) and the issue order of every
+ * system (issue [n_sys][issue_cap] of node << 16 | packed instruction, issue_n[n_sys]). */
+int orc_run_packed_ex(int np, const uint16_t *traces, const uint32_t *counts, uint32_t stride,
+                      uint64_t n_sys, uint32_t ring_cap, uint64_t sched_seed,
+                      uint32_t sched_thresh, uint64_t first_sys, dsm_res *res, dsm_rec *dump,
+                      dsm_rec *fin, uint32_t *issue, uint32_t issue_cap, uint32_t *issue_n,
+                      int nthreads);
+
 /* Fill traces [sys][node][n_instr] and counts [sys][node] from the generator. */
 void orc_generate(int np, int dist, uint64_t seed, uint32_t n_instr, uint64_t first_sys,
                   uint64_t n_sys, uint16_t *traces, uint32_t *counts);

@@ -24,6 +24,15 @@ outputs.  Nothing written here is reference source text.
   tests/golden/ensemble/<name>_recs.npy        first 16 systems' dump + final node records
                                                uint8 [16, 2, np, 64]
   tests/golden/ensemble/meta.json              generator parameters per fixture
+  tests/golden/lockstep/<test>/instruction_order.txt
+                                               the reference's own DEBUG_INSTR issue lines
+                                               (:595-598) under the lock-step schedule
+                                               (oracle/_ref/ref_lockstep_np4_i32_dbg)
+  tests/golden/explore/<test>.npy              per-system results [K, 6] of K seeded
+                                               schedule-exploration variants (seed 7, act
+                                               threshold 0x8000) of the reference's handler
+                                               text (oracle/_ref/ref_lockstep_np4_i32)
+  tests/golden/explore/issue_md5.json          md5 of each variant's DEBUG_INSTR issue lines
   tests/golden/dumps/random_recs.npy           4096 seeded random node records (uint8 [n, 64],
                                                every field in its valid range; record k is
                                                node k % 8)
@@ -35,6 +44,7 @@ import concurrent.futures as cf
 import hashlib
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -165,6 +175,41 @@ def ensemble():
         json.dump(meta, f, indent=1, sort_keys=True)
 
 
+EXPLORE_K, EXPLORE_SEED, EXPLORE_THRESH = 256, 7, 0x8000
+ISSUE_RE = re.compile(rb"^Processor \d+: instr type=.*\n", re.M)
+
+
+def explore():
+    d = os.path.join(GOLD, "explore")
+    os.makedirs(d, exist_ok=True)
+    issue = {}
+    for t in TESTS:
+        with tempfile.TemporaryDirectory() as tmp:
+            os.symlink(os.path.join(GOLD, "inputs"), os.path.join(tmp, "tests"))
+            dbg = os.path.join(REFBIN, "ref_lockstep_np4_i32_dbg")
+            out = subprocess.run([dbg, "tests", t, "res.bin"], cwd=tmp, check=True,
+                                 capture_output=True).stdout
+            with open(os.path.join(GOLD, "lockstep", t, "instruction_order.txt"), "wb") as f:
+                f.write(b"".join(ISSUE_RE.findall(out)))
+            args = [t, "res.bin", str(EXPLORE_SEED), hex(EXPLORE_THRESH), "0", str(EXPLORE_K)]
+            subprocess.run([os.path.join(REFBIN, "ref_lockstep_np4_i32"), "tests"] + args,
+                           cwd=tmp, check=True, stdout=subprocess.DEVNULL)
+            res, _ = read_ref_bin(os.path.join(tmp, "res.bin"), 4)
+            np.save(os.path.join(d, f"{t}.npy"), res_to_u64(res))
+            out = subprocess.run([dbg, "tests"] + args, cwd=tmp, check=True,
+                                 capture_output=True).stdout
+            lines = ISSUE_RE.findall(out)
+            k, md5s = 0, []
+            for r in res:
+                md5s.append(md5(b"".join(lines[k:k + int(r["instrs"])])))
+                k += int(r["instrs"])
+            assert k == len(lines)
+            issue[t] = md5s
+    with open(os.path.join(d, "issue_md5.json"), "w") as f:
+        json.dump({"k": EXPLORE_K, "seed": EXPLORE_SEED, "thresh": EXPLORE_THRESH,
+                   "issue_md5": issue}, f, indent=0)
+
+
 def random_records(n, seed):
     """Node records with every field in its valid range; cache states uniform over the four
     (so about a quarter of the cache lines print the 9-character "EXCLUSIVE")."""
@@ -205,7 +250,7 @@ if __name__ == "__main__":
     if not os.path.exists(os.path.join(REF, "assignment.c")) or \
             not os.path.exists(os.path.join(REFBIN, "ref_lockstep_np8")):
         sys.exit("gen_fixtures: needs /root/reference and oracle/_ref (make -C oracle ref)")
-    steps = sys.argv[1:] or ["inputs", "lockstep", "observed", "ensemble", "dumps"]
+    steps = sys.argv[1:] or ["inputs", "lockstep", "observed", "ensemble", "dumps", "explore"]
     for s in steps:
         print("gen_fixtures:", s, flush=True)
         globals()[s]()

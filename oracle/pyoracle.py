@@ -29,6 +29,8 @@ def lib():
         L.orc_run_system.argtypes = [i32, vp, vp, u32, u32, vp, vp, vp, vp]
         L.orc_run_packed.argtypes = [i32, vp, vp, u32, u64, u32, vp, vp, vp, vp, i32]
         L.orc_run_generated.argtypes = [i32, i32, u64, u32, u64, u64, u32, vp, vp, i32]
+        L.orc_run_packed_ex.argtypes = [i32, vp, vp, u32, u64, u32, u64, u32, u64, vp, vp, vp, vp,
+                                        u32, vp, i32]
         L.orc_generate.argtypes = [i32, i32, u64, u32, u64, u64, vp, vp]
         L.orc_generate.restype = None
         L.orc_format_dump.argtypes = [i32, vp, ctypes.c_char_p, i32]
@@ -55,6 +57,39 @@ def run_packed(np_, traces, counts, ring_cap=256, nthreads=8, records=False):
                               _p(fin), _p(bt), nthreads)
     assert rc == 0
     return res, bt, dump, fin
+
+
+LOCKSTEP = 0x10000
+
+
+def run_packed_ex(np_, traces, counts, sched_seed=0, sched_thresh=LOCKSTEP, first_sys=0,
+                  ring_cap=256, nthreads=8, issue=False):
+    """run_packed with seeded schedule exploration (system id first_sys + i in the schedule
+    hash) and, with issue=True, the issue order: (res, dump, fin, events [n, cap], n_events)."""
+    traces = np.ascontiguousarray(traces, dtype=np.uint16)
+    counts = np.ascontiguousarray(counts, dtype=np.uint32)
+    n, _, stride = traces.shape
+    res = np.zeros(n, dtype=RES_DT)
+    dump = np.zeros((n, np_, 64), dtype=np.uint8)
+    fin = np.zeros((n, np_, 64), dtype=np.uint8)
+    cap = np_ * stride
+    ev = np.zeros((n, cap), dtype=np.uint32) if issue else None
+    evn = np.zeros(n, dtype=np.uint32) if issue else None
+    rc = lib().orc_run_packed_ex(np_, _p(traces), _p(counts), stride, n, ring_cap, sched_seed,
+                                 sched_thresh, first_sys, _p(res), _p(dump), _p(fin), _p(ev), cap,
+                                 _p(evn), nthreads)
+    assert rc == 0
+    return res, dump, fin, ev, evn
+
+
+def issue_lines(events):
+    """DEBUG_INSTR lines (assignment.c:596-597) of one system's issue order."""
+    out = []
+    for e in events:
+        node, ins = int(e) >> 16, int(e) & 0xFFFF
+        out.append("Processor %d: instr type=%c, address=0x%02X, value=%d\n"
+                   % (node, "W" if ins >> 15 else "R", (ins >> 8) & 0x7F, ins & 0xFF))
+    return "".join(out)
 
 
 def run_generated(np_, dist, seed, n_instr, first, n, ring_cap=256, nthreads=8):

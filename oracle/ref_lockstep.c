@@ -20,6 +20,8 @@
  * Usage:
  *   ref_lockstep tests <name> <out.bin>      (CWD must contain tests/<name>/core_n.txt;
  *                                            dumps written to CWD by printProcessorState)
+ *   ref_lockstep tests <name> <out.bin> <seed> <thresh> <first> <n>
+ *                                            (n seeded schedule-exploration variants; no files)
  *   ref_lockstep gen <dist> <seed> <n_instr> <first_sys> <n_sys> <out.bin>
  *   ref_lockstep fmt <recs.bin> <out.bin>   (printProcessorState of 64-byte records)
  *   ref_lockstep bench <dist> <seed> <n_instr> <first> <n> <nproc>
@@ -143,6 +145,10 @@ static void reset_ctx(int t) {
     C[t].node.outstandingMsgs = 0;
 }
 
+/* seeded schedule exploration (dsm_common.h dsm_sched_act); lock-step by default */
+static uint64_t g_sched_seed, g_sys;
+static uint32_t g_sched_thresh = DSM_SCHED_LOCKSTEP;
+
 static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
     uint32_t rounds = 0, msgs = 0, instrs = 0, status = ST_COMPLETED;
     g_assert_failed = 0;
@@ -151,6 +157,14 @@ static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
         nst = 0;
         for (int t = 0; t < NUM_PROCS; ++t) {
             nodeCtx *c = &C[t];
+            if (g_sched_thresh < DSM_SCHED_LOCKSTEP) {
+                const int avail = c->count > 0 ||
+                    (!(c->node.waitingForReply > 0) && !c->instructions_done);
+                if (avail && !dsm_sched_act(g_sched_seed, g_sched_thresh, g_sys, r, t)) {
+                    acted = 1;
+                    continue;
+                }
+            }
             if (c->count > 0) {
                 message m = c->ring[c->head];
                 c->head = (c->head + 1) % MSG_BUFFER_SIZE;
@@ -211,6 +225,25 @@ static void write_sys(FILE *f, const dsm_res *res, const dsm_rec *dump, const ds
 int main(int argc, char **argv) {
     dsm_res res;
     dsm_rec dump[NUM_PROCS], fin[NUM_PROCS];
+    if (argc == 8 && !strcmp(argv[1], "tests")) {
+        /* n schedule-exploration variants (system ids first .. first+n-1) of one test */
+        g_sched_seed = strtoull(argv[4], 0, 0);
+        g_sched_thresh = (uint32_t)strtoul(argv[5], 0, 0);
+        const uint64_t first = strtoull(argv[6], 0, 0), n = strtoull(argv[7], 0, 0);
+        FILE *f = fopen(argv[3], "wb");
+        if (!f) { perror("open out"); return 1; }
+        for (uint64_t k = 0; k < n; ++k) {
+            g_sys = first + k;
+            for (int t = 0; t < NUM_PROCS; ++t) {
+                reset_ctx(t);
+                initializeProcessor(t, &C[t].node, argv[2]);
+            }
+            run_system(&res, dump, fin);
+            write_sys(f, &res, dump, fin);
+        }
+        fclose(f);
+        return 0;
+    }
     if (argc == 4 && !strcmp(argv[1], "tests")) {
         FILE *f = fopen(argv[3], "wb");
         if (!f) { perror("open out"); return 1; }
