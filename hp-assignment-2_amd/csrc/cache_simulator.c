@@ -19,6 +19,10 @@
  *   --max-instr N    instructions read per core file, default 32 (MAX_INSTR_NUM, :13)
  *   --device D       GPU ordinal, default 0
  *   --quiet          do not print the "initialized" lines
+ *   --issue-order F  write the issue order to file F in the reference's DEBUG_INSTR format
+ *                    (:595-598), as the schedule issued the instructions
+ *   --schedule S:T   seeded schedule exploration (dsm_set_schedule): seed S, act threshold T
+ *                    (0..65536; 65536 = lock-step); samples the reference's interleavings
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -27,18 +31,25 @@
 #include "dsm.h"
 
 static void usage(const char *argv0) {
-    fprintf(stderr, "Usage: %s [--np 4|8] [--max-instr N] [--device D] <test_directory>\n", argv0);
+    fprintf(stderr, "Usage: %s [--np 4|8] [--max-instr N] [--device D] [--quiet] [--issue-order FILE]\n"
+                    "          [--schedule SEED:THRESH] <test_directory>\n", argv0);
 }
 
 int main(int argc, char **argv) {
     int np = 4, device = 0, quiet = 0;
     uint32_t max_instr = DSM_REF_MAX_INSTR;
-    const char *dir = NULL;
+    const char *dir = NULL, *issue_file = NULL;
+    unsigned long long sched_seed = 0;
+    unsigned sched_thresh = DSM_SCHED_LOCKSTEP;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--np") && i + 1 < argc) np = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--max-instr") && i + 1 < argc) max_instr = (uint32_t)atoi(argv[++i]);
         else if (!strcmp(argv[i], "--device") && i + 1 < argc) device = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--quiet")) quiet = 1;
+        else if (!strcmp(argv[i], "--issue-order") && i + 1 < argc) issue_file = argv[++i];
+        else if (!strcmp(argv[i], "--schedule") && i + 1 < argc) {
+            if (sscanf(argv[++i], "%llu:%u", &sched_seed, &sched_thresh) != 2) { usage(argv[0]); return EXIT_FAILURE; }
+        }
         else if (argv[i][0] == '-' && argv[i][1] == '-') { usage(argv[0]); return EXIT_FAILURE; }
         else dir = argv[i];
     }
@@ -78,7 +89,7 @@ int main(int argc, char **argv) {
     memset(&cfg, 0, sizeof cfg);
     cfg.np = np;
     cfg.max_instr = stride;
-    cfg.flags = DSM_F_SNAPSHOTS;
+    cfg.flags = DSM_F_SNAPSHOTS | (issue_file ? DSM_F_ISSUE_TRACE : 0u);
     dsm_ctx *ctx = NULL;
     int rc = dsm_open(device, &cfg, &ctx);
     if (rc) {
@@ -106,6 +117,10 @@ int main(int argc, char **argv) {
     fflush(stdout);
     free(text);
 
+    if ((rc = dsm_set_schedule(ctx, sched_seed, sched_thresh))) {
+        fprintf(stderr, "Error: dsm_set_schedule: %s\n", dsm_strerror(rc));
+        return EXIT_FAILURE;
+    }
     dsm_sys_result res;
     rc = dsm_run_packed(ctx, traces, counts, 1, &res, NULL);
     if (rc) {
@@ -114,6 +129,22 @@ int main(int argc, char **argv) {
         return EXIT_FAILURE;
     }
     const uint32_t status = res.status & 0xFFu, dumped = res.status >> 8;
+    if (issue_file) {                                   /* DEBUG_INSTR order, :595-598 */
+        uint32_t n = 0, cap = (uint32_t)np * stride;
+        uint32_t *ev = (uint32_t *)malloc(cap * sizeof(uint32_t));
+        char *txt = (char *)malloc((size_t)cap * 64 + 1);
+        FILE *f = NULL;
+        if (!ev || !txt || (rc = dsm_get_issue_trace(ctx, 0, ev, cap, &n)) ||
+            (rc = dsm_format_issue_trace(ev, n < cap ? n : cap, txt, (size_t)cap * 64 + 1)) < 0 ||
+            !(f = fopen(issue_file, "w")) || fwrite(txt, 1, (size_t)rc, f) != (size_t)rc) {
+            fprintf(stderr, "Error: issue order: %s\n", rc < 0 ? dsm_strerror(rc) : "write failed");
+            dsm_close(ctx);
+            return EXIT_FAILURE;
+        }
+        fclose(f);
+        free(ev);
+        free(txt);
+    }
     /* printProcessorState of every node that finished issuing (:695), formatted on the GPU */
     if ((rc = dsm_write_run_dumps(ctx, 0, dumped, NULL))) {
         fprintf(stderr, "Error: dumps: %s\n", dsm_strerror(rc));

@@ -58,6 +58,11 @@ struct SimArgs {
     uint32_t *ovf_list;             /* fast kernel: systems handed to the 256-deep re-run   */
     unsigned int *ovf_count;
     const uint2 *table;             /* micro-op table (dsm_table.h), DT_ENTRIES entries     */
+    uint64_t sched_seed;            /* M_SX: seeded schedule exploration (dsm_set_schedule)  */
+    uint32_t sched_thresh;
+    uint32_t issue_cap;             /* M_TR: events per system                               */
+    uint32_t *issue;                /* M_TR: [sys][issue_cap] node << 16 | packed instruction */
+    uint32_t *issue_n;              /* M_TR: [sys] events                                    */
 };
 
 
@@ -203,14 +208,22 @@ DEVI uint32_t gather4(uint32_t x, uint32_t r) {
  * predicates, selects): a divergent 17-way switch costs every wave the sum of the taken
  * cases plus their exec-mask bookkeeping.  Only the once-per-node dump, the trace-chunk
  * refill and the per-system finish are real branches.                                   */
-template <int NP, int RING, int WAVES, bool GEN, bool TC, int OCC = 5>
+/* MODE bits: the optional parts of a round, compiled in only where asked for */
+enum : int {
+    M_TC = 1,   /* per-type message counters (DSM_F_TYPE_COUNTS): 16-bit fields per node and
+                 * system, added to the wave counters when the system finishes             */
+    M_TR = 2,   /* issue-order trace (DSM_F_ISSUE_TRACE): DEBUG_INSTR order, :595-598      */
+    M_SX = 4    /* seeded schedule exploration (dsm_set_schedule): a node with an action
+                 * may stall for the round (oracle/dsm_common.h dsm_sched_act)            */
+};
+
+template <int NP, int RING, int WAVES, bool GEN, int MODE, int OCC = 5>
 __global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
 sim_kernel(const SimArgs *Ap) {
     constexpr int GPW = 64 / NP;
     constexpr uint32_t NPM = (1u << NP) - 1u;
     constexpr bool FB = (RING == FB_RING);   /* the 256-deep re-run kernel                */
-    /* TC: per-type message counters (DSM_F_TYPE_COUNTS), 16-bit fields per node and
-     * system, added to the wave counters when the system finishes (exact per system). */
+    constexpr bool TC = (MODE & M_TC) != 0, TR = (MODE & M_TR) != 0, SX = (MODE & M_SX) != 0;
 
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
     __shared__ uint32_t s_ring[WAVES][RING][64];                       /* inbox rings   */
@@ -242,6 +255,9 @@ sim_kernel(const SimArgs *Ap) {
     uint32_t rounds = 0, rmsg = 0;
     bool live = false;
     uint32_t tc[7] = {0, 0, 0, 0, 0, 0, 0};                                  /* TC only */
+    uint32_t nev = 0;                          /* TR: issue events of the system so far */
+    const uint64_t smul = SX ? Ap->sched_seed * 0x9E3779B97F4A7C15ULL : 0;
+    const uint32_t sthr = SX ? Ap->sched_thresh : 0;
     nd.dst = nd.caddr = nd.cval = nd.cst = nd.ctl = nd.ip = nd.nins = nd.rh = nd.nmsg = 0;
 
     /* initializeProcessor :778-790 and main :142-146 for a new system in this lane's group */
@@ -253,6 +269,7 @@ sim_kernel(const SimArgs *Ap) {
         nd.dst = 0xAAAAAAAAu; nd.caddr = 0xFFFFFFFFu; nd.cval = 0; nd.cst = 0xFFu;
         nd.ctl = 0; nd.ip = 0; nd.rh = 0; nd.nmsg = 0;
         rounds = 0;
+        nev = 0;
         if (TC) {
 #pragma unroll
             for (int k = 0; k < 7; ++k) tc[k] = 0;
@@ -284,10 +301,20 @@ sim_kernel(const SimArgs *Ap) {
 
         /* ---- (1) this round's action, from state at the start of the round ---------- */
         const uint32_t cnt0 = nd.rh >> 8, head0 = nd.rh & 0xFFu;
-        const bool hasMsg = live && cnt0 != 0;                            /* :158-169 */
+        bool hasMsg = live && cnt0 != 0;                                  /* :158-169 */
         const bool canIssue = live && !hasMsg && !(nd.ctl & C_WAIT);      /* :578-581 */
-        const bool doIssue = canIssue && nd.ip < nd.nins;                 /* :590-592 */
-        const bool doDump = canIssue && !doIssue && !(nd.ctl & C_DUMPED); /* :688-697 */
+        bool doIssue = canIssue && nd.ip < nd.nins;                       /* :590-592 */
+        bool doDump = canIssue && !doIssue && !(nd.ctl & C_DUMPED);       /* :688-697 */
+        bool stall = false;
+        if (SX) {           /* a node with an action may stall this round (dsm_sched_act) */
+            const bool avail = hasMsg || doIssue || doDump;
+            const uint64_t key = (sys << 26) ^ ((uint64_t)(rounds + 1) << 3) ^ (uint64_t)node;
+            const uint32_t h = (uint32_t)(splitmix(smul + key) >> 48);
+            stall = avail && h >= sthr;
+            hasMsg = hasMsg && !stall;
+            doIssue = doIssue && !stall;
+            doDump = doDump && !stall;
+        }
         /* trace refill: when this round's issue takes the last instruction of `cur`, the
          * chunk after `nxt` is requested NOW and rotated in at the end of the round, so its
          * HBM latency overlaps this round's transition and delivery (a load consumed in the
@@ -307,8 +334,14 @@ sim_kernel(const SimArgs *Ap) {
                 ins = (k & 1u) ? (d >> 16) : (d & 0xFFFFu);
             }
             w = ((ins >> 15) ? OP_WR : OP_RD) | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
+            if (TR) {                  /* the group's issues of this round, in node order */
+                const uint32_t g = (uint32_t)(__ballot(true) >> gbase) & NPM;
+                const uint32_t pos = nev + __builtin_popcount(g & ((1u << node) - 1u));
+                if (pos < Ap->issue_cap) Ap->issue[sys * Ap->issue_cap + pos] = (node << 16) | ins;
+            }
             nd.ip++;
         }
+        if (TR) nev += __builtin_popcount((uint32_t)(__ballot(doIssue) >> gbase) & NPM);
         const uint32_t op = (hasMsg || doIssue) ? (w & 15u) : doDump ? OP_DUMP : OP_IDLE;
 
         /* ---- (2) decode, then the micro-op table (dsm_table.h) ------------------------ */
@@ -391,7 +424,7 @@ sim_kernel(const SimArgs *Ap) {
         }
 
         /* ---- (5) per-system termination (Appendix A step 4) -------------------------- */
-        const uint64_t actb = __ballot(op != OP_IDLE);
+        const uint64_t actb = __ballot(op != OP_IDLE || stall);    /* stalled = available */
         const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
         const uint32_t gact = (uint32_t)(actb >> gbase) & NPM;
         const bool gbad = ((badb >> gbase) & NPM) != 0;
@@ -423,6 +456,7 @@ sim_kernel(const SimArgs *Ap) {
                     } else {
                         reinterpret_cast<uint4 *>(Ap->results)[2 * sys] =
                             make_uint4(st | (dmask << 8), rounds, msgs, ins);
+                        if (TR) Ap->issue_n[sys] = nev;
                         atomicAdd(&s_cnt[wv][K_MSGS], (unsigned long long)msgs);
                         atomicAdd(&s_cnt[wv][K_INSTRS], (unsigned long long)ins);
                         atomicAdd(&s_cnt[wv][K_ROUNDS], (unsigned long long)rounds);
@@ -595,37 +629,54 @@ typedef void (*sim_fn)(const SimArgs *);
 /* Waves per workgroup of the fast transition kernel.  The micro-op table is one copy per
  * workgroup in LDS; at ring 12 a wave needs ~6 KB of LDS and the kernel fits 5 waves per
  * SIMD (96 VGPRs), so 4-wave groups (5 per CU = 20 waves, 146 KB LDS) fill the CU where
- * 8-wave groups stop at 2 per CU (16 waves).  DSM_FW=4|8 selects it for A/B runs. */
-struct FastK { sim_fn fn; int waves; };
-static int fw_choice() {
-    const char *e = getenv("DSM_FW");
-    const int v = e ? atoi(e) : 4;
-    return v == 8 ? 8 : 4;
-}
-template <int NP, bool GEN, bool TC, int W>
-sim_fn fast_kernel(int ring) {
+ * 8-wave groups stop at 2 per CU (16 waves; measured 0.6% slower, profiles/README.md). */
+constexpr int FW = 4;
+
+template <int NP, bool GEN, int MODE>
+sim_fn fast_mode(int ring) {
+    /* the inbox depth only moves time, never results: every depth for the bench mode, and
+     * the overflow-prone depth 4 (which exercises the 256-deep re-run) for the others */
     switch (ring) {
-    case 4: return sim_kernel<NP, 4, W, GEN, TC>;
-    case 8: return sim_kernel<NP, 8, W, GEN, TC>;
-    case 16: return sim_kernel<NP, 16, W, GEN, TC>;
-    default: return sim_kernel<NP, 12, W, GEN, TC>;
+    case 4: return sim_kernel<NP, 4, FW, GEN, MODE>;
+    case 8: if (MODE == 0) return sim_kernel<NP, 8, FW, GEN, 0>; break;
+    case 16: if (MODE == 0) return sim_kernel<NP, 16, FW, GEN, 0>; break;
+    default: break;
+    }
+    return sim_kernel<NP, 12, FW, GEN, MODE>;
+}
+template <int NP, bool GEN>
+sim_fn fast_np_gen(int ring, int mode) {
+    switch (mode) {
+    case 1: return fast_mode<NP, GEN, 1>(ring);
+    case 2: return fast_mode<NP, GEN, 2>(ring);
+    case 3: return fast_mode<NP, GEN, 3>(ring);
+    case 4: return fast_mode<NP, GEN, 4>(ring);
+    case 5: return fast_mode<NP, GEN, 5>(ring);
+    case 6: return fast_mode<NP, GEN, 6>(ring);
+    case 7: return fast_mode<NP, GEN, 7>(ring);
+    default: return fast_mode<NP, GEN, 0>(ring);
     }
 }
-template <int NP, bool GEN>
-FastK fast_np_gen(int ring, bool tc) {
-    if (fw_choice() == 8)
-        return {tc ? fast_kernel<NP, GEN, true, 8>(ring) : fast_kernel<NP, GEN, false, 8>(ring), 8};
-    return {tc ? fast_kernel<NP, GEN, true, 4>(ring) : fast_kernel<NP, GEN, false, 4>(ring), 4};
-}
-FastK pick_fast(int np, int ring, bool gen, bool tc) {
-    if (np == 4) return gen ? fast_np_gen<4, true>(ring, tc) : fast_np_gen<4, false>(ring, tc);
-    return gen ? fast_np_gen<8, true>(ring, tc) : fast_np_gen<8, false>(ring, tc);
+sim_fn pick_fast(int np, int ring, bool gen, int mode) {
+    if (np == 4) return gen ? fast_np_gen<4, true>(ring, mode) : fast_np_gen<4, false>(ring, mode);
+    return gen ? fast_np_gen<8, true>(ring, mode) : fast_np_gen<8, false>(ring, mode);
 }
 template <int NP, bool GEN>
-sim_fn fb_np_gen(bool tc) { return tc ? sim_kernel<NP, FB_RING, 1, GEN, true, 1> : sim_kernel<NP, FB_RING, 1, GEN, false, 1>; }
-sim_fn pick_fallback(int np, bool gen, bool tc) {
-    if (np == 4) return gen ? fb_np_gen<4, true>(tc) : fb_np_gen<4, false>(tc);
-    return gen ? fb_np_gen<8, true>(tc) : fb_np_gen<8, false>(tc);
+sim_fn fb_np_gen(int mode) {
+    switch (mode) {
+    case 1: return sim_kernel<NP, FB_RING, 1, GEN, 1, 1>;
+    case 2: return sim_kernel<NP, FB_RING, 1, GEN, 2, 1>;
+    case 3: return sim_kernel<NP, FB_RING, 1, GEN, 3, 1>;
+    case 4: return sim_kernel<NP, FB_RING, 1, GEN, 4, 1>;
+    case 5: return sim_kernel<NP, FB_RING, 1, GEN, 5, 1>;
+    case 6: return sim_kernel<NP, FB_RING, 1, GEN, 6, 1>;
+    case 7: return sim_kernel<NP, FB_RING, 1, GEN, 7, 1>;
+    default: return sim_kernel<NP, FB_RING, 1, GEN, 0, 1>;
+    }
+}
+sim_fn pick_fallback(int np, bool gen, int mode) {
+    if (np == 4) return gen ? fb_np_gen<4, true>(mode) : fb_np_gen<4, false>(mode);
+    return gen ? fb_np_gen<8, true>(mode) : fb_np_gen<8, false>(mode);
 }
 int lds_bytes(int ring, int waves) {
     return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 2 + K_N * 8) + DT_ENTRIES * 8;
@@ -671,6 +722,7 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     if (!c) return DSM_E_NOMEM;
     c->device = device;
     c->cfg = *cfg;
+    c->sched_thresh = DSM_SCHED_LOCKSTEP;
     c->ring = ring;
     c->cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -705,7 +757,7 @@ extern "C" void dsm_close(dsm_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *ptrs[] = {c->d_ctrl, c->d_args, c->d_partials, c->d_ovf_list, c->d_traces, c->d_counts,
-                    c->d_res, c->d_cnt, c->d_recs, c->d_table};
+                    c->d_res, c->d_cnt, c->d_recs, c->d_table, c->d_issue, c->d_issue_n};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     dsm_text_release(c);
     if (c->h_args) (void)hipHostFree(c->h_args);
@@ -730,10 +782,10 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     if (n_sys > 0xFFFFFFFFull) return DSM_E_INVAL;
     HIPCK(hipSetDevice(c->device));
     const int np = c->cfg.np, gpw = 64 / np;
-    const bool tc = (c->cfg.flags & DSM_F_TYPE_COUNTS) != 0;
-    const FastK fk = pick_fast(np, c->ring, gen, tc);
-    const sim_fn fast = fk.fn, fb = pick_fallback(np, gen, tc);
-    const int FW = fk.waves;
+    const bool tr = (c->cfg.flags & DSM_F_ISSUE_TRACE) != 0;
+    const int mode = ((c->cfg.flags & DSM_F_TYPE_COUNTS) ? M_TC : 0) | (tr ? M_TR : 0) |
+                     (c->sched_thresh < DSM_SCHED_LOCKSTEP ? M_SX : 0);
+    const sim_fn fast = pick_fast(np, c->ring, gen, mode), fb = pick_fallback(np, gen, mode);
     int nb_fast = 0, nb_fb = 0;
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fast, (const void *)fast, 64 * FW, 0));
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fb, (const void *)fb, 64, 0));
@@ -777,6 +829,17 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.ovf_list = c->d_ovf_list;
     A.ovf_count = c->d_ctrl + CTRL_OVF;
     A.table = c->d_table;
+    A.sched_seed = c->sched_seed;
+    A.sched_thresh = c->sched_thresh;
+    if (tr) {
+        const size_t cap = (size_t)np * c->cfg.max_instr;
+        if ((rc = ensure(&c->d_issue, &c->issue_cap_total, (size_t)n_sys * cap))) return rc;
+        if ((rc = ensure(&c->d_issue_n, &c->issue_n_cap, (size_t)n_sys))) return rc;
+        A.issue = c->d_issue;
+        A.issue_n = c->d_issue_n;
+        A.issue_cap = (uint32_t)cap;
+        c->issue_sys = n_sys;
+    }
     SimArgs &B = c->h_args[1];
     B = A;
     B.d_n = c->d_ctrl + CTRL_OVF;
@@ -813,7 +876,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     c->info.block_threads = 64 * FW;
     c->info.waves_per_cu = nb_fast * FW;
     c->info.cus = c->cus;
-    c->info.ring_cap = c->ring;
+    c->info.ring_cap = (mode && c->ring != 4) ? 12 : c->ring;
     c->info.lds_bytes_per_block = lds_bytes(c->ring, FW);
     return DSM_OK;
 }
@@ -926,5 +989,29 @@ extern "C" int dsm_get_node_state(dsm_ctx *c, uint64_t sys, int node, dsm_node_s
     const size_t i = ((size_t)sys * c->cfg.np + node) * 8;
     if (dump) HIPCK(hipMemcpy(dump, c->d_recs + i, sizeof *dump, hipMemcpyDeviceToHost));
     if (final_state) HIPCK(hipMemcpy(final_state, c->d_recs + i + 4, sizeof *final_state, hipMemcpyDeviceToHost));
+    return DSM_OK;
+}
+
+extern "C" int dsm_set_schedule(dsm_ctx *c, uint64_t seed, uint32_t act_thresh) {
+    if (!c) return DSM_E_INVAL;
+    c->sched_seed = seed;
+    c->sched_thresh = act_thresh >= DSM_SCHED_LOCKSTEP ? DSM_SCHED_LOCKSTEP : act_thresh;
+    return DSM_OK;
+}
+
+extern "C" int dsm_get_issue_trace(dsm_ctx *c, uint64_t sys, uint32_t *events, uint32_t cap,
+                                   uint32_t *n) {
+    if (!c || !n || (cap && !events)) return DSM_E_INVAL;
+    if (!(c->cfg.flags & DSM_F_ISSUE_TRACE) || !c->d_issue) return DSM_E_STATE;
+    if (sys >= c->issue_sys) return DSM_E_INVAL;
+    HIPCK(hipSetDevice(c->device));
+    HIPCK(hipStreamSynchronize(c->stream));
+    HIPCK(hipDeviceSynchronize());
+    uint32_t k = 0;
+    HIPCK(hipMemcpy(&k, c->d_issue_n + sys, sizeof k, hipMemcpyDeviceToHost));
+    const uint32_t per = (uint32_t)(c->cfg.np * c->cfg.max_instr);
+    const uint32_t m = k < cap ? k : cap;
+    if (m) HIPCK(hipMemcpy(events, c->d_issue + sys * per, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *n = k;
     return DSM_OK;
 }

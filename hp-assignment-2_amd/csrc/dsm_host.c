@@ -126,6 +126,20 @@ int dsm_write_dump(int node, const dsm_node_state *st, const char *dir) {
     return (w == (size_t)len && rc == 0) ? DSM_OK : DSM_E_IO;
 }
 
+int dsm_format_issue_trace(const uint32_t *events, uint32_t n, char *buf, size_t cap) {
+    if ((n && !events) || !buf) return DSM_E_INVAL;
+    size_t k = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t e = events[i], ins = e & 0xFFFFu;
+        const int w = snprintf(buf + k, cap - k, "Processor %u: instr type=%c, address=0x%02X, value=%u\n",
+                               e >> 16, (ins >> 15) ? 'W' : 'R', (ins >> 8) & 0x7Fu, ins & 0xFFu);
+        if (w < 0 || (size_t)w >= cap - k) return DSM_E_INVAL;                /* :596-597 */
+        k += (size_t)w;
+    }
+    if (k < cap) buf[k] = 0;
+    return (int)k;
+}
+
 static uint64_t fmix64(uint64_t z) {
     z ^= z >> 33; z *= 0xff51afd7ed558ccdULL;
     z ^= z >> 33; z *= 0xc4ceb9fe1a85ec53ULL;

@@ -39,6 +39,13 @@ struct dsm_ctx {
     hipEvent_t ev0, ev1, ev_args;
     int timed;
     dsm_launch_info info;
+    uint64_t sched_seed;             /* dsm_set_schedule                                     */
+    uint32_t sched_thresh;
+    uint32_t *d_issue;               /* DSM_F_ISSUE_TRACE: [sys][np * max_instr] events      */
+    size_t issue_cap_total;
+    uint32_t *d_issue_n;
+    size_t issue_n_cap;
+    uint64_t issue_sys;
     /* dsm_text.hip */
     uint4 *d_dump_tpl;               /* np printProcessorState templates, DSM_DUMP_SLOT each  */
     char *d_text_tmp;                /* small staging for host-side dump writes              */

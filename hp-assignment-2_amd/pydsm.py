@@ -22,6 +22,8 @@ DIST = {"uniform": 0, "hot": 1, "evict": 2}
 F_SNAPSHOTS = 1
 F_TIMING = 2
 F_TYPE_COUNTS = 4
+F_ISSUE_TRACE = 8
+SCHED_LOCKSTEP = 0x10000
 
 RESULT_DTYPE = np.dtype([("status", "<u4"), ("rounds", "<u4"), ("msgs", "<u4"),
                          ("instrs", "<u4"), ("dump_hash", "<u8"), ("final_hash", "<u8")])
@@ -98,6 +100,9 @@ def lib():
             "dsm_format_dumps_device": (i32, [vp, vp, u32, u64, vp, vp, vp]),
             "dsm_format_run_dumps_device": (i32, [vp, i32, u64, u64, vp, vp, vp]),
             "dsm_write_run_dumps": (i32, [vp, u64, u32, ctypes.c_char_p]),
+            "dsm_set_schedule": (i32, [vp, u64, u32]),
+            "dsm_get_issue_trace": (i32, [vp, u64, vp, u32, ctypes.POINTER(u32)]),
+            "dsm_format_issue_trace": (i32, [vp, u32, ctypes.c_char_p, ctypes.c_size_t]),
             "dsm_parse_traces_device": (i32, [vp, vp, vp, u64, u32, vp, vp, vp, vp]),
             "dsm_parse_traces": (i32, [vp, vp, vp, u64, u32, vp, vp, vp]),
             "dsm_generate_text_device": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp, vp]),
@@ -140,12 +145,13 @@ class Engine:
     """One dsm_ctx: np nodes per system, trace stride max_instr, bound to `device`."""
 
     def __init__(self, np_=8, max_instr=4096, ring_cap=0, snapshots=False, device=0, timing=False,
-                 type_counts=False):
+                 type_counts=False, issue_trace=False):
         self.np = np_
         self.max_instr = max_instr
         self.cfg = Config(np_, max_instr, ring_cap,
                           (F_SNAPSHOTS if snapshots else 0) | (F_TIMING if timing else 0) |
-                          (F_TYPE_COUNTS if type_counts else 0))
+                          (F_TYPE_COUNTS if type_counts else 0) |
+                          (F_ISSUE_TRACE if issue_trace else 0))
         self.ctx = ctypes.c_void_p()
         _check(lib().dsm_open(device, ctypes.byref(self.cfg), ctypes.byref(self.ctx)), "dsm_open")
 
@@ -263,6 +269,18 @@ class Engine:
                                          out_dir.encode() if out_dir else None),
                "dsm_write_run_dumps")
 
+    # -- schedule exploration / issue order --------------------------------------------------
+    def set_schedule(self, seed, act_thresh=SCHED_LOCKSTEP):
+        _check(lib().dsm_set_schedule(self.ctx, seed, act_thresh), "dsm_set_schedule")
+
+    def issue_trace(self, sys):
+        cap = self.np * self.max_instr
+        ev = np.zeros(cap, dtype=np.uint32)
+        n = ctypes.c_uint32(0)
+        _check(lib().dsm_get_issue_trace(self.ctx, sys, _ptr(ev), cap, ctypes.byref(n)),
+               "dsm_get_issue_trace")
+        return ev[:min(n.value, cap)].copy()
+
     def last_kernel_ms(self):
         ms = ctypes.c_float(0)
         _check(lib().dsm_last_kernel_ms(self.ctx, ctypes.byref(ms)), "dsm_last_kernel_ms")
@@ -297,6 +315,16 @@ def split_dumps(text, lens):
     """Bulk GPU dump buffer (uint8, DUMP_SLOT bytes per record) + lengths -> list of str."""
     text = np.asarray(text, dtype=np.uint8).reshape(-1, DUMP_SLOT)
     return [bytes(text[k, :int(n)]).decode() for k, n in enumerate(np.asarray(lens))]
+
+
+def format_issue_trace(events):
+    events = np.ascontiguousarray(events, dtype=np.uint32)
+    cap = 64 * max(len(events), 1) + 1
+    buf = ctypes.create_string_buffer(cap)
+    n = lib().dsm_format_issue_trace(_ptr(events), len(events), buf, cap)
+    if n < 0:
+        raise DsmError(n, "dsm_format_issue_trace")
+    return buf.raw[:n].decode()
 
 
 def node_hash(node, rec, nwords):

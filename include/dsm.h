@@ -88,6 +88,10 @@ enum { DSM_VIEW_DUMP = 0,   /* snapshot when the node finished issuing (:695)   
 #define DSM_F_SNAPSHOTS 1u  /* keep per-node dump + final records of the last run          */
 #define DSM_F_TIMING 2u     /* record HIP events around the transition kernel of each run     */
 #define DSM_F_TYPE_COUNTS 4u /* count handled messages per transactionType (msgs_by_type)     */
+#define DSM_F_ISSUE_TRACE 8u /* record every system's issue order (dsm_get_issue_trace)         */
+
+/* act_thresh of dsm_set_schedule that means the plain lock-step schedule (the default) */
+#define DSM_SCHED_LOCKSTEP 0x10000u
 
 typedef struct dsm_config {
     int np;              /* NUM_PROCS: 4 or 8                                               */
@@ -198,6 +202,25 @@ int dsm_run_generated(dsm_ctx *ctx, const dsm_gen *gen, uint64_t first_sys, uint
  * `final_state` = state when the system stopped.  Either pointer may be NULL. */
 int dsm_get_node_state(dsm_ctx *ctx, uint64_t sys, int node, dsm_node_state *dump,
                        dsm_node_state *final_state);
+
+/* Seeded schedule exploration for the following runs: in each round, a node that has an
+ * action (Appendix A: inbox head, issue, dump) takes it only if the top 16 bits of
+ * splitmix64(seed * 0x9E3779B97F4A7C15 + (sys << 26 ^ round << 3 ^ node)) are below
+ * act_thresh, else it stalls that round -- another legal interleaving of the reference's
+ * free-running OpenMP threads (:153-699).  A round counts while any node has an action.
+ * act_thresh >= DSM_SCHED_LOCKSTEP restores the lock-step schedule.  sys is the system's
+ * index in the run. */
+int dsm_set_schedule(dsm_ctx *ctx, uint64_t seed, uint32_t act_thresh);
+
+/* Issue order of system `sys` of the last run (needs DSM_F_ISSUE_TRACE): events in the
+ * order the reference's DEBUG_INSTR printf (:595-598) would print them under the schedule
+ * (round, then node): node << 16 | packed instruction.  *n = number of events (may exceed
+ * cap; min(cap, *n) are copied). */
+int dsm_get_issue_trace(dsm_ctx *ctx, uint64_t sys, uint32_t *events, uint32_t cap,
+                        uint32_t *n);
+/* DEBUG_INSTR lines ("Processor %d: instr type=%c, address=0x%02X, value=%d\n") of n
+ * events; returns the length, or DSM_E_INVAL if cap is too small (host only). */
+int dsm_format_issue_trace(const uint32_t *events, uint32_t n, char *buf, size_t cap);
 
 /* Device time of the transition kernel of the last run (needs DSM_F_TIMING): HIP events
  * recorded on the run's own stream right before and after the kernel launch.  Waits for
