@@ -48,7 +48,7 @@ constexpr uint32_t SLOT = DSM_DUMP_SLOT, SLOT16 = DSM_DUMP_SLOT / 16;
 constexpr uint32_t MEM0 = 193, MEML = 31;     /* "|  %3d  |  0x%02X   |  %5d   |\n"      :846 */
 constexpr uint32_t DIR0 = 856, DIRL = 45;     /* "|  %3d  |  0x%02X   |  %2s   |   0x%08X   |\n" :856 */
 constexpr uint32_t CAC0 = 1748, CACL = 41;    /* "|  %3d  |  0x%02X   |  %3d  |  %8s \t|\n" :867 */
-constexpr uint32_t ITEMS = 16 + 16 + 4;       /* memory, directory, cache lines per record */
+constexpr uint32_t ITEMS = 16 + 16 + 15;      /* memory, directory, cache-section pieces */
 
 DEVI char hexu(uint32_t d) { return (char)(d < 10 ? '0' + d : 'A' + d - 10); }
 /* %3d of 0..255 */
@@ -59,31 +59,54 @@ DEVI void dec3(char *p, uint32_t v) {
 }
 
 /* FR records per workgroup iteration, NT threads per workgroup */
-template <uint32_t FR, uint32_t NT>
+template <uint32_t FR, uint32_t NT, bool TLDS>
 __global__ void __launch_bounds__(NT) fmt_kernel(const uint8_t *recs, uint64_t rec_stride,
                                                  uint64_t n, int np, const uint4 *tpl,
                                                  v4u32 *out, uint32_t *lens) {
+    /* TLDS: the np node-id templates live in LDS for the whole kernel (copied once), so a
+     * record's text starts from an LDS-to-LDS copy instead of an L2 read, and the next tile's
+     * records are fetched into registers while this tile's slots stream out. */
     __shared__ uint4 s_buf[FR * SLOT16];
     __shared__ uint32_t s_rec[FR][16];
+    __shared__ uint4 s_tpl[TLDS ? DSM_MAX_NP * SLOT16 : 1];
     char *const sb = reinterpret_cast<char *>(s_buf);
     const uint32_t tid = threadIdx.x;
+    if (TLDS) {
+        for (uint32_t i = tid; i < (uint32_t)np * SLOT16; i += NT) s_tpl[i] = tpl[i];
+    }
+    uint4 rv = make_uint4(0, 0, 0, 0);          /* TLDS: this thread's share of the records */
+    auto fetch = [&](uint64_t b) {
+        const uint32_t nr = (n - b) < FR ? (uint32_t)(n - b) : FR;
+        if (tid < nr * 4)
+            rv = *reinterpret_cast<const uint4 *>(recs + (b + (tid >> 2)) * rec_stride + (tid & 3u) * 16);
+    };
+    if (TLDS && (uint64_t)blockIdx.x * FR < n) fetch((uint64_t)blockIdx.x * FR);
     for (uint64_t base = (uint64_t)blockIdx.x * FR; base < n; base += (uint64_t)gridDim.x * FR) {
         const uint32_t nr = (n - base) < FR ? (uint32_t)(n - base) : FR;
         /* (1) node-id template (static text + node-dependent address column) and records */
+        if (TLDS) __syncthreads();                       /* s_tpl ready / last tile stored */
         for (uint32_t i = tid; i < nr * SLOT16; i += NT) {
             const uint32_t r = i / SLOT16, c = i - r * SLOT16;
-            s_buf[i] = tpl[(uint32_t)((base + r) % (uint64_t)np) * SLOT16 + c];
+            const uint32_t t = (uint32_t)((base + r) % (uint64_t)np) * SLOT16 + c;
+            s_buf[i] = TLDS ? s_tpl[t] : tpl[t];
         }
         if (tid < nr * 4) {
             const uint32_t r = tid >> 2, q = tid & 3u;
-            const uint4 v = *reinterpret_cast<const uint4 *>(recs + (base + r) * rec_stride + q * 16);
+            const uint4 v = TLDS ? rv : *reinterpret_cast<const uint4 *>(recs + (base + r) * rec_stride + q * 16);
             s_rec[r][4 * q + 0] = v.x; s_rec[r][4 * q + 1] = v.y;
             s_rec[r][4 * q + 2] = v.z; s_rec[r][4 * q + 3] = v.w;
         }
         __syncthreads();
+        if (TLDS && base + (uint64_t)gridDim.x * FR < n) fetch(base + (uint64_t)gridDim.x * FR);
         /* (2) one work item per variable field group */
-        for (uint32_t i = tid; i < nr * ITEMS; i += NT) {
-            const uint32_t r = i / ITEMS, f = i - r * ITEMS;
+        /* items ordered type-major (all memory fields of the tile, then directory, then cache
+         * pieces), so a wave's iteration runs one item type: no divergence across types */
+        for (uint32_t i = tid; i < FR * ITEMS; i += NT) {
+            uint32_t r, f;
+            if (i < 16 * FR) { r = i >> 4; f = i & 15u; }
+            else if (i < 32 * FR) { r = (i - 16 * FR) >> 4; f = 16 + ((i - 16 * FR) & 15u); }
+            else { r = (i - 32 * FR) / 15u; f = 32 + (i - 32 * FR) % 15u; }
+            if (r >= nr) continue;
             const uint8_t *rb = reinterpret_cast<const uint8_t *>(s_rec[r]);
             char *t = sb + r * SLOT;
             if (f < 16) {                                        /* node.memory[f], %5d */
@@ -95,28 +118,47 @@ __global__ void __launch_bounds__(NT) fmt_kernel(const uint8_t *recs, uint64_t r
                 l[22] = st == 0 ? 'M' : st == 1 ? 'S' : st == 2 ? 'U' : '?';
                 l[38] = hexu(bv >> 4);                           /* 0x%08X of a byte */
                 l[39] = hexu(bv & 15u);
-            } else {                                             /* cache[k]: whole line */
-                const uint32_t k = f - 32;
-                uint32_t sh = 0;
-                for (uint32_t j = 0; j < k; ++j) sh += rb[56 + j] == 1;   /* "EXCLUSIVE" */
-                char *l = t + CAC0 + CACL * k + sh;
-                const uint32_t a = rb[48 + k], v = rb[52 + k], st = rb[56 + k];
-                l[0] = '|'; l[1] = ' '; l[2] = ' '; l[3] = ' '; l[4] = ' ';
-                l[5] = (char)('0' + k); l[6] = ' '; l[7] = ' '; l[8] = '|'; l[9] = ' ';
-                l[10] = ' '; l[11] = '0'; l[12] = 'x'; l[13] = hexu(a >> 4); l[14] = hexu(a & 15u);
-                l[15] = ' '; l[16] = ' '; l[17] = ' '; l[18] = '|'; l[19] = ' '; l[20] = ' ';
-                dec3(l + 21, v);
-                l[24] = ' '; l[25] = ' '; l[26] = '|'; l[27] = ' '; l[28] = ' ';
-                /* %8s of cacheStateStr[state] (:826) */
-                const char *s8 = st == 0 ? "MODIFIED" : st == 1 ? "EXCLUSIVE"
-                               : st == 2 ? "  SHARED" : st == 3 ? " INVALID" : "    ????";
-                const uint32_t w = st == 1 ? 9u : 8u;
-                for (uint32_t j = 0; j < w; ++j) l[29 + j] = s8[j];
-                char *e = l + 29 + w;
-                e[0] = ' '; e[1] = '\t'; e[2] = '|'; e[3] = '\n';
-                if (k == 3) {                                    /* section trailer :870 */
-                    for (uint32_t j = 0; j < 40; ++j) e[4 + j] = '-';
-                    e[44] = '\n'; e[45] = '\n';
+            } else {
+                /* cache section (:865-870): 3 items per line + 3 for the trailer.  The
+                 * template holds the all-MODIFIED layout; "EXCLUSIVE" is one character longer,
+                 * so a line after an EXCLUSIVE one (and the trailer) moves and is rewritten
+                 * whole, while an unmoved line only gets its fields. */
+                const uint32_t q = f - 32;
+                const uint32_t em = (rb[56] == 1) | ((rb[57] == 1) << 1) | ((rb[58] == 1) << 2) | ((rb[59] == 1) << 3);
+                if (q < 12) {
+                    const uint32_t k = q / 3, part = q - 3 * k;
+                    const uint32_t sh = __builtin_popcount(em & ((1u << k) - 1u));
+                    const bool moved = sh != 0;
+                    char *l = t + CAC0 + CACL * k + sh;
+                    if (part == 0) {                          /* "|  %3d  |  0x%02X" */
+                        const uint32_t a = rb[48 + k];
+                        if (moved) {
+                            l[0] = '|'; l[1] = ' '; l[2] = ' '; l[3] = ' '; l[4] = ' ';
+                            l[5] = (char)('0' + k); l[6] = ' '; l[7] = ' '; l[8] = '|';
+                            l[9] = ' '; l[10] = ' '; l[11] = '0'; l[12] = 'x';
+                        }
+                        l[13] = hexu(a >> 4); l[14] = hexu(a & 15u);
+                    } else if (part == 1) {                   /* "   |  %3d  |  " */
+                        if (moved) {
+                            l[15] = ' '; l[16] = ' '; l[17] = ' '; l[18] = '|'; l[19] = ' '; l[20] = ' ';
+                            l[24] = ' '; l[25] = ' '; l[26] = '|'; l[27] = ' '; l[28] = ' ';
+                        }
+                        dec3(l + 21, rb[52 + k]);
+                    } else {                                  /* "%8s \t|\n" */
+                        const uint32_t st = rb[56 + k];
+                        const char *s8 = st == 0 ? "MODIFIED" : st == 1 ? "EXCLUSIVE"
+                                       : st == 2 ? "  SHARED" : st == 3 ? " INVALID" : "    ????";
+                        const uint32_t w = st == 1 ? 9u : 8u;
+                        for (uint32_t j = 0; j < w; ++j) l[29 + j] = s8[j];
+                        if (moved || st == 1) {
+                            char *e = l + 29 + w;
+                            e[0] = ' '; e[1] = '\t'; e[2] = '|'; e[3] = '\n';
+                        }
+                    }
+                } else if (em) {                              /* trailer moved: 3 x 14 bytes */
+                    char *e = t + CAC0 + 4 * CACL + __builtin_popcount(em);
+                    const uint32_t j0 = 14u * (q - 12);
+                    for (uint32_t j = j0; j < j0 + 14u; ++j) e[j] = j < 40u ? '-' : '\n';
                 }
             }
         }
@@ -133,7 +175,7 @@ __global__ void __launch_bounds__(NT) fmt_kernel(const uint8_t *recs, uint64_t r
             y.x = x.x; y.y = x.y; y.z = x.z; y.w = x.w;
             __builtin_nontemporal_store(y, dst + i);
         }
-        __syncthreads();
+        if (!TLDS) __syncthreads();
     }
 }
 
@@ -470,13 +512,14 @@ static int ensure_templates(dsm_ctx *c) {
     return DSM_OK;
 }
 
-/* Workgroup tile of fmt_kernel: DSM_FMT=16|8|4 records per iteration (256 / 128 / 64
- * threads) for A/B runs; smaller tiles put more independent copy-patch-store pipelines on
- * each CU. */
+/* Workgroup tile of fmt_kernel: DSM_FMT=FR (4, 8, 16: records per iteration, templates read
+ * from L2) or 100 + FR (108, 116, 132: templates resident in LDS, next tile's records
+ * prefetched) for A/B runs.  Measured on 8M records (tools/ab_fmt.py): 16 5.47 ms, 116 3.40,
+ * 132 3.35 (5.1 TB/s) -- the default. */
 static int fmt_choice() {
     const char *e = getenv("DSM_FMT");
-    const int v = e ? atoi(e) : 16;
-    return (v == 4 || v == 8) ? v : 16;
+    const int v = e ? atoi(e) : 132;
+    return (v == 4 || v == 8 || v == 16 || v == 108 || v == 116) ? v : 132;   /* 1xx: LDS templates */
 }
 
 static int launch_fmt(dsm_ctx *c, const uint8_t *recs, uint64_t stride_bytes, uint64_t n,
@@ -484,21 +527,23 @@ static int launch_fmt(dsm_ctx *c, const uint8_t *recs, uint64_t stride_bytes, ui
     if (n == 0) return DSM_OK;
     int rc = ensure_templates(c);
     if (rc) return rc;
-    const int fr = fmt_choice();
+    const int v = fmt_choice(), fr = v % 100;
+    const bool tl = v >= 100;
+    const void *fn = tl ? (fr == 8 ? (const void *)fmt_kernel<8, 128, true>
+                           : fr == 32 ? (const void *)fmt_kernel<32, 512, true> : (const void *)fmt_kernel<16, 256, true>)
+                        : fr == 4 ? (const void *)fmt_kernel<4, 64, false>
+                        : fr == 8 ? (const void *)fmt_kernel<8, 128, false> : (const void *)fmt_kernel<16, 256, false>;
+    const int nt = fr == 4 ? 64 : fr == 8 ? 128 : fr == 32 ? 512 : 256;
+    int per_cu = 0;
+    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, 0));
+    if (per_cu < 1) per_cu = 1;
     uint64_t blocks = (n + fr - 1) / fr;
-    const uint64_t cap = (uint64_t)c->cus * (64 / fr) * 4;   /* 4 waves' worth per CU per tile size */
+    const uint64_t cap = (uint64_t)c->cus * per_cu;             /* one resident round */
     if (blocks > cap) blocks = cap;
     const uint4 *tpl = (const uint4 *)c->d_dump_tpl;
     v4u32 *out = (v4u32 *)d_text;
-    if (fr == 4)
-        hipLaunchKernelGGL((fmt_kernel<4, 64>), dim3((unsigned)blocks), dim3(64), 0, st, recs,
-                           stride_bytes, n, c->cfg.np, tpl, out, d_len);
-    else if (fr == 8)
-        hipLaunchKernelGGL((fmt_kernel<8, 128>), dim3((unsigned)blocks), dim3(128), 0, st, recs,
-                           stride_bytes, n, c->cfg.np, tpl, out, d_len);
-    else
-        hipLaunchKernelGGL((fmt_kernel<16, 256>), dim3((unsigned)blocks), dim3(256), 0, st, recs,
-                           stride_bytes, n, c->cfg.np, tpl, out, d_len);
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(const uint8_t *, uint64_t, uint64_t, int, const uint4 *, v4u32 *, uint32_t *)>(const_cast<void *>(fn)),
+                       dim3((unsigned)blocks), dim3(nt), 0, st, recs, stride_bytes, n, c->cfg.np, tpl, out, d_len);
     HIPCK(hipGetLastError());
     return DSM_OK;
 }

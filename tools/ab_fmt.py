@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import pydsm  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8 << 20
-variants = (sys.argv[2] if len(sys.argv) > 2 else "16,8,4").split(",")
+variants = (sys.argv[2] if len(sys.argv) > 2 else "16,8,116,108").split(",")
 reps = 5
 dev = torch.device("cuda", 0)
 st = torch.cuda.current_stream(dev)
