@@ -17,9 +17,9 @@
  *     byte select over 8 registers;
  *   - inboxes: LDS rings s_ring[wave][slot][lane] (bank = lane % 32, conflict-free);
  *   - a round: every lane takes one action (predicated data flow, no per-type branches),
- *     writes <= 2 outgoing words + their destination masks to LDS; each receiver gathers
- *     the masks of its group with one ds_read_b128 and appends the words addressed to it in
- *     ascending (sender, word) order -- the reference's (sender, program order) delivery;
+ *     writes <= 2 outgoing words to LDS and ORs their bits into the receivers' receive masks
+ *     (LDS atomics); each receiver appends the words addressed to it in ascending
+ *     (sender, word) order -- the reference's (sender, program order) delivery;
  *   - per-system termination by wave ballot; finished systems are replaced from sharded
  *     device work counters (persistent kernel), so lanes never idle on a long-tail system;
  *   - traces are read as 16-byte chunks per lane (current + prefetched next) from HBM;
@@ -196,11 +196,6 @@ DEVI uint4 ld16(const uint16_t *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-/* gather bit `r` of each of the 4 bytes of x into bits 0..3 */
-DEVI uint32_t gather4(uint32_t x, uint32_t r) {
-    const uint32_t t = (x >> r) & 0x01010101u;
-    return (t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu;
-}
 
 /* ---- the transition kernel ------------------------------------------------------------ *
  * One loop iteration = one lock-step round of every system resident in the wave.  The 13
@@ -228,13 +223,14 @@ sim_kernel(const SimArgs *Ap) {
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
     __shared__ uint32_t s_ring[WAVES][RING][64];                       /* inbox rings   */
     __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][128]; /* 2 words/lane  */
-    __shared__ __attribute__((aligned(16))) uint16_t s_dm[WAVES][64];   /* dest masks    */
+    __shared__ uint32_t s_rm[WAVES][64];                               /* receive masks */
     __shared__ unsigned long long s_cnt[WAVES][K_N];
     __shared__ uint2 s_tab[DT_ENTRIES];                                /* micro-op table */
 
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t node = lane % NP, gbase = lane - node;
     if (lane < K_N) s_cnt[wv][lane] = 0;
+    s_rm[wv][lane] = 0;
     for (uint32_t i = threadIdx.x; i < DT_ENTRIES; i += 64 * WAVES) s_tab[i] = Ap->table[i];
     __syncthreads();
 
@@ -386,17 +382,20 @@ sim_kernel(const SimArgs *Ap) {
         /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         reinterpret_cast<uint2 *>(s_out[wv])[lane] = make_uint2(o0, o1);
-        s_dm[wv][lane] = (uint16_t)((o0 >> 24) | ((o1 >> 24) << 8));
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t R;                      /* bit 2*sender+word: that word is addressed to me */
-        if (NP == 8) {
-            const uint4 x = *reinterpret_cast<const uint4 *>(&s_dm[wv][gbase]);
-            R = gather4(x.x, node) | (gather4(x.y, node) << 4) | (gather4(x.z, node) << 8) |
-                (gather4(x.w, node) << 12);
-        } else {
-            const uint2 x = *reinterpret_cast<const uint2 *>(&s_dm[wv][gbase]);
-            R = gather4(x.x, node) | (gather4(x.y, node) << 4);
+        /* receive masks, transposed at the sender: word j of this node sets bit 2*node + j of
+         * every destination's mask (LDS atomic OR; a multicast INV visits its destinations in
+         * a short loop), so a receiver reads its mask instead of gathering bits from the
+         * group's destination bytes */
+        {
+            uint32_t m0 = o0 >> 24, m1 = o1 >> 24;
+            if (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], 1u << (2 * node)); m0 &= m0 - 1; }
+            if (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], 2u << (2 * node)); m1 &= m1 - 1; }
+            while (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], 1u << (2 * node)); m0 &= m0 - 1; }
+            while (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], 2u << (2 * node)); m1 &= m1 - 1; }
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        uint32_t R = s_rm[wv][lane];     /* bit 2*sender+word: that word is addressed to me */
+        s_rm[wv][lane] = 0;
         {
             const uint32_t hh = nd.rh & 0xFFu;
             uint32_t cc = nd.rh >> 8;
@@ -679,7 +678,7 @@ sim_fn pick_fallback(int np, bool gen, int mode) {
     return gen ? fb_np_gen<8, true>(mode) : fb_np_gen<8, false>(mode);
 }
 int lds_bytes(int ring, int waves) {
-    return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 2 + K_N * 8) + DT_ENTRIES * 8;
+    return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 4 + K_N * 8) + DT_ENTRIES * 8;
 }
 
 }  // namespace

@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdsm.so")
+LIB_PATH = os.environ.get("DSM_LIB") or os.path.join(HERE, "libdsm.so")   # DSM_LIB: A/B builds
 CLI_PATH = os.path.join(HERE, "cache_simulator")
 
 NTYPES = 13
