@@ -23,8 +23,11 @@
  *
  * An entry (64 bits) says what to do with the cache line, the directory entry, the memory
  * byte, the two outgoing message words (templates whose operands are picked from a few
- * runtime values), waitingForReply, pendingWriteValue and the assert flag; three bits
+ * runtime values), waitingForReply, pendingWriteValue and the assert flag; a few bits
  * gate parts of it on `line->address == 0xFF`, the only condition left out of C.
+ * dt_entry states each handler as micro-op bits (E_*); dt_compile turns them into what the
+ * datapath reads: a byte-permute selector (W0) for the four byte results and packed fields
+ * (W1).
  */
 #ifndef DSM_TABLE_H
 #define DSM_TABLE_H
@@ -221,11 +224,61 @@ static inline void dt_entry(uint32_t opx, uint32_t sub, uint32_t *lo_out, uint32
     *hi_out = h;
 }
 
-/* the whole table: tab[2 * i] = low word, tab[2 * i + 1] = high word */
+/* ---- compiled entry: what the datapath reads ------------------------------------------
+ * W0 is a v_perm_b32 selector over the candidate bytes
+ *     X = {a, v, La, Lv} (bytes 0-3),  Y = {pend, Mv, Db, Db & ~sbit} (bytes 4-7), 12 = 0x00
+ * producing the bytes {new line.address, new line.value, new memory byte, first word's
+ * payload} in one instruction.  W1 holds the remaining fields (layout below).           */
+enum : uint32_t {
+    DP_A = 0, DP_V = 1, DP_LA = 2, DP_LV = 3, DP_PEND = 4, DP_MV = 5, DP_DB = 6, DP_EVDB = 7,
+    DP_ZERO = 12
+};
+#define W1_DBASE(x) ((uint32_t)(x) << 0)   /* dir bv base: 0 bv, 1 bv & ~sbit, 2 zero        */
+#define W1_ORS (1u << 2)                   /* | 1 << sender                                  */
+#define W1_ORR (1u << 3)                   /* | 1 << secondReceiver                          */
+#define W1_LS (1u << 4)                    /* line.state = LSV (bits 5-6)                    */
+#define W1_DS (1u << 7)                    /* dir state = DSV (bits 8-9)                     */
+#define W1_O0 (1u << 10)                   /* first word: type bits 11-14                    */
+#define W1_O0LA (1u << 15)                 /*   address = line.address (victim), else a      */
+#define W1_R2(x) ((uint32_t)(x) << 16)     /*   r2 field: 0 zero, 1 sender, 2 secondReceiver */
+#define W1_X (1u << 18)                    /*   exclusive flag                               */
+#define W1_DEST(x) ((uint32_t)(x) << 19)   /*   destination code (E_O0D)                     */
+#define W1_O1(x) ((uint32_t)(x) << 22)     /* second word: 0 none, 1 RREQ, 2 WREQ, 3 UPGRADE  */
+#define W1_O1V (1u << 24)                  /*   payload v                                    */
+#define W1_WSET (1u << 25)
+#define W1_WCLR (1u << 26)
+#define W1_PEND (1u << 27)
+#define W1_ASSERT (1u << 28)
+#define W1_O0NFF (1u << 29)                /* first word only if line.address != 0xFF        */
+#define W1_FFG (1u << 30)                  /* assert only, line/wait effects only, if line.address == 0xFF resp. not */
+
+static inline void dt_compile(uint32_t e, uint32_t h, uint32_t *w0, uint32_t *w1) {
+    static const uint32_t lv_sel[4] = {DP_LV, DP_V, DP_PEND, DP_ZERO};    /* E_LV codes  */
+    static const uint32_t pay_sel[4] = {DP_ZERO, DP_MV, DP_EVDB, DP_LV};  /* E_O0P codes */
+    *w0 = ((e & E_LA) ? DP_A : DP_LA) | (lv_sel[(e >> 1) & 3u] << 8) |
+          (((e & E_MEM) ? DP_V : DP_MV) << 16) | (pay_sel[(e >> 20) & 3u] << 24);
+    const uint32_t t1 = (h >> 8) & 15u;
+    const uint32_t o1 = !(e & E_O1) ? 0u : t1 == DT_RREQ ? 1u : t1 == DT_WREQ ? 2u : 3u;
+    *w1 = W1_DBASE((e & E_DBANDS) ? 1u : (e & E_DBAND0) ? 2u : 0u) |
+          ((e & E_DBORS) ? W1_ORS : 0u) | ((e & E_DBORR) ? W1_ORR : 0u) |
+          ((e & E_LS) ? W1_LS : 0u) | (((e >> 4) & 3u) << 5) |
+          ((e & E_DS) ? W1_DS : 0u) | (((e >> 11) & 3u) << 8) |
+          ((e & E_O0) ? W1_O0 : 0u) | (((e >> 15) & 15u) << 11) | ((e & E_O0LA) ? W1_O0LA : 0u) |
+          W1_R2((e & E_O0RS) ? 1u : (e & E_O0RR) ? 2u : 0u) | ((e & E_O0X) ? W1_X : 0u) |
+          W1_DEST((e >> 25) & 7u) | W1_O1(o1) | ((e & E_O1V) ? W1_O1V : 0u) |
+          ((h & E_WSET) ? W1_WSET : 0u) | ((h & E_WCLR) ? W1_WCLR : 0u) |
+          ((e & E_PEND) ? W1_PEND : 0u) | ((h & E_ASSERT) ? W1_ASSERT : 0u) |
+          ((h & E_O0NFF) ? W1_O0NFF : 0u) | ((h & (E_ANFF | E_LINEFF)) ? W1_FFG : 0u);
+}
+
+/* the whole table, compiled: tab[2 * i] = W0, tab[2 * i + 1] = W1 */
 static inline void dt_build(uint32_t *tab) {
     for (uint32_t op = 0; op < DT_NOPS; ++op)
-        for (uint32_t sub = 0; sub < DT_STRIDE; ++sub)
-            dt_entry(op, sub, &tab[2 * (op * DT_STRIDE + sub)], &tab[2 * (op * DT_STRIDE + sub) + 1]);
+        for (uint32_t sub = 0; sub < DT_STRIDE; ++sub) {
+            uint32_t e, h;
+            dt_entry(op, sub, &e, &h);
+            dt_compile(e, h, &tab[2 * (op * DT_STRIDE + sub)], &tab[2 * (op * DT_STRIDE + sub) + 1]);
+        }
 }
 
 /* ---- the datapath (host + device) ----------------------------------------------------- */
@@ -269,42 +322,63 @@ DSM_HD uint32_t dt_index(const DtIn &in, uint32_t *evDb_out, uint32_t *own_out) 
     return opx * DT_STRIDE + sub;
 }
 
-DSM_HD DtOut dt_apply(const DtIn &in, uint32_t E0, uint32_t E1, uint32_t evDb, uint32_t own) {
+/* v_perm_b32: byte i of the result = byte sel_i of {hi (bytes 4-7), lo (bytes 0-3)}; 12 = 0 */
+DSM_HD uint32_t dt_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t k = (sel >> (8 * i)) & 0xFFu;
+        const uint32_t b = k < 8u ? (uint32_t)(v >> (8 * k)) & 0xFFu : (k == 12u ? 0u : 0xFFu);
+        r |= b << (8 * i);
+    }
+    return r;
+#endif
+}
+
+DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb, uint32_t own) {
     DtOut o;
     const uint32_t H = in.a >> 4, sbit = 1u << in.s;
     const bool laFF = (in.La == 0xFFu);
-    const bool lineOn = !(E1 & E_LINEFF) || laFF;
-    /* cache line */
-    o.nLa = (lineOn && (E0 & E_LA)) ? in.a : in.La;
-    const bool lv0 = lineOn && (E0 & E_LV(1)), lv1 = lineOn && (E0 & E_LV(2));
-    o.nLv = lv1 ? (lv0 ? 0u : in.pend) : (lv0 ? in.v : in.Lv);
-    o.nLs = (lineOn && (E0 & E_LS)) ? ((E0 >> 4) & 3u) : in.Ls;
-    /* directory entry: bv = (bv & AND) | OR */
-    const uint32_t andm = (E0 & E_DBANDS) ? ~sbit : (E0 & E_DBAND0) ? 0u : 0xFFu;
-    const uint32_t orm = ((E0 & E_DBORS) ? sbit : 0u) | ((E0 & E_DBORR) ? (1u << in.r2) : 0u);
-    o.nDb = (in.Db & andm & 0xFFu) | orm;
-    o.nDs = (E0 & E_DS) ? ((E0 >> 11) & 3u) : in.Ds;
-    o.nMv = (E0 & E_MEM) ? in.v : in.Mv;
+    const bool lineOn = !(W1 & W1_FFG) || laFF;
+    /* the four byte outputs in one byte permute; line effects off = keep La, Lv */
+    const uint32_t sel = lineOn ? W0 : ((W0 & 0xFFFF0000u) | (DP_LV << 8) | DP_LA);
+    const uint32_t X = in.a | (in.v << 8) | (in.La << 16) | (in.Lv << 24);
+    const uint32_t Y = in.pend | (in.Mv << 8) | (in.Db << 16) | ((evDb & 0xFFu) << 24);
+    const uint32_t P = dt_perm(Y, X, sel);
+    o.nLa = P & 0xFFu;
+    o.nLv = (P >> 8) & 0xFFu;
+    o.nMv = (P >> 16) & 0xFFu;
+    const uint32_t pay = P >> 24;
+    /* cache line state, directory entry */
+    o.nLs = (lineOn && (W1 & W1_LS)) ? ((W1 >> 5) & 3u) : in.Ls;
+    const uint32_t db = W1 & 3u;
+    const uint32_t base = (db & 2u) ? 0u : (db ? (evDb & 0xFFu) : in.Db);
+    o.nDb = base | ((W1 & W1_ORS) ? sbit : 0u) | ((W1 & W1_ORR) ? (1u << in.r2) : 0u);
+    o.nDs = (W1 & W1_DS) ? ((W1 >> 8) & 3u) : in.Ds;
     /* first outgoing word */
-    const bool p0 = E0 & E_O0P(1), p1 = E0 & E_O0P(2);
-    const uint32_t pay = p1 ? (p0 ? in.Lv : (evDb & 0xFFu)) : (p0 ? in.Mv : 0u);
-    const uint32_t r2f = (E0 & E_O0RS) ? in.s : (E0 & E_O0RR) ? in.r2 : 0u;
-    const bool d0 = E0 & E_O0D(1), d1 = E0 & E_O0D(2), d2 = E0 & E_O0D(4);
+    const uint32_t rc = (W1 >> 16) & 3u;
+    const uint32_t r2f = (rc & 2u) ? in.r2 : (rc ? in.s : 0u);
+    const uint32_t dc = (W1 >> 19) & 7u;
+    const bool d0 = dc & 1u, d1 = dc & 2u, d2 = dc & 4u;
     const uint32_t ctzEv = (uint32_t)__builtin_ctz((evDb & in.np_mask) | 0x80000000u);
     const uint32_t didx = d1 ? (d0 ? ctzEv : (in.La >> 4)) : (d0 ? own : in.s);
     const uint32_t mset = d0 ? (in.v & in.np_mask & ~(1u << in.node)) : ((1u << H) | (1u << in.r2));
     const uint32_t dm = d2 ? mset : (1u << didx);
-    const bool on0 = (E0 & E_O0) && (!(E1 & E_O0NFF) || !laFF);
-    const uint32_t addr0 = (E0 & E_O0LA) ? in.La : in.a;
-    o.o0 = on0 ? (((E0 >> 15) & 15u) | (addr0 << 4) | (pay << 11) | (r2f << 19) |
-                  (((E0 >> 24) & 1u) << 22) | (dm << 24)) : 0u;
-    /* second outgoing word: the request to the home */
-    o.o1 = (E0 & E_O1) ? (((E1 >> 8) & 15u) | (in.a << 4) | (((E0 & E_O1V) ? in.v : 0u) << 11) |
-                          (1u << (24 + H))) : 0u;
-    o.wset = lineOn && (E1 & E_WSET);
-    o.wclr = lineOn && (E1 & E_WCLR);
-    o.pendw = (E0 & E_PEND) != 0u;
-    o.asrt = (E1 & E_ASSERT) && (!(E1 & E_ANFF) || !laFF);
+    const bool on0 = (W1 & W1_O0) && (!(W1 & W1_O0NFF) || !laFF);
+    const uint32_t addr0 = (W1 & W1_O0LA) ? in.La : in.a;
+    o.o0 = on0 ? (((W1 >> 11) & 15u) | (addr0 << 4) | (pay << 11) | (r2f << 19) |
+                  (((W1 >> 18) & 1u) << 22) | (dm << 24)) : 0u;
+    /* second outgoing word: the request to the home (type RREQ 0 / WREQ 1 / UPGRADE 6) */
+    const uint32_t c1 = (W1 >> 22) & 3u;
+    o.o1 = c1 ? (((0x6100u >> (4 * c1)) & 15u) | (in.a << 4) | (((W1 & W1_O1V) ? in.v : 0u) << 11) |
+                 (1u << (24 + H))) : 0u;
+    o.wset = lineOn && (W1 & W1_WSET);
+    o.wclr = lineOn && (W1 & W1_WCLR);
+    o.pendw = (W1 & W1_PEND) != 0u;
+    o.asrt = (W1 & W1_ASSERT) && (!(W1 & W1_FFG) || !laFF);
     return o;
 }
 
