@@ -90,17 +90,7 @@ constexpr uint64_t NO_SYS = ~0ull;
 constexpr int FB_RING = 256;        /* MSG_BUFFER_SIZE, assignment.c:12 */
 
 /* ---- small bit-field helpers ------------------------------------------------------- */
-/* Runtime selection among 4 register words, written as masks: a ?: chain over array
- * elements gets folded into a runtime-indexed load, which sends the array to scratch. */
-DEVI uint32_t msk(bool b) { return 0u - (uint32_t)b; }
-DEVI uint32_t sel4(const uint32_t (&w)[4], uint32_t q) {
-    return (w[0] & msk(q == 0)) | (w[1] & msk(q == 1)) | (w[2] & msk(q == 2)) | (w[3] & msk(q == 3));
-}
 DEVI uint32_t get8(uint32_t w, uint32_t i) { return __builtin_amdgcn_ubfe(w, i * 8, 8); }
-DEVI uint32_t set8(uint32_t w, uint32_t i, uint32_t v) {
-    const uint32_t sh = i * 8;
-    return (w & ~(0xFFu << sh)) | (v << sh);
-}
 DEVI uint32_t get2(uint32_t w, uint32_t i) { return __builtin_amdgcn_ubfe(w, i * 2, 2); }
 DEVI uint32_t set2(uint32_t w, uint32_t i, uint32_t v) {
     const uint32_t sh = i * 2;
@@ -326,8 +316,12 @@ sim_kernel(const SimArgs *Ap) {
             if (GEN) {
                 ins = gen_instr<NP>(gmul, gdist, gfirst + sys, node, nd.ip);
             } else {
-                const uint32_t k = nd.ip & 7u, d = sel4(cur, k >> 1);
-                ins = (k & 1u) ? (d >> 16) : (d & 0xFFFFu);
+                /* `cur` is a 128-bit shift register: the next instruction is its low half-word */
+                ins = cur[0] & 0xFFFFu;
+                cur[0] = __builtin_amdgcn_alignbit(cur[1], cur[0], 16);
+                cur[1] = __builtin_amdgcn_alignbit(cur[2], cur[1], 16);
+                cur[2] = __builtin_amdgcn_alignbit(cur[3], cur[2], 16);
+                cur[3] >>= 16;
             }
             w = ((ins >> 15) ? OP_WR : OP_RD) | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
             if (TR) {                  /* the group's issues of this round, in node order */
@@ -356,8 +350,11 @@ sim_kernel(const SimArgs *Ap) {
         const uint32_t o0 = o.o0, o1 = o.o1;
 
         /* ---- (3) write back (idle lanes rewrite unchanged values) ------------------- */
-        nd.caddr = set8(nd.caddr, idx, o.nLa);
-        nd.cval = set8(nd.cval, idx, o.nLv);
+        {   /* line.address / line.value bytes 0 / 1 of o.P into byte idx of caddr / cval */
+            const uint32_t sa = 0x03020100u + ((4u - idx) << (8 * idx));
+            nd.caddr = __builtin_amdgcn_perm(o.P, nd.caddr, sa);
+            nd.cval = __builtin_amdgcn_perm(o.P, nd.cval, sa + (1u << (8 * idx)));
+        }
         nd.cst = set2(nd.cst, idx, o.nLs);
         nd.dst = set2(nd.dst, blk, o.nDs);
         *mbp = (uint16_t)(o.nMv | (o.nDb << 8));

@@ -292,11 +292,21 @@ struct DtIn {
 };
 struct DtOut {
     uint32_t nLa, nLv, nLs, nDb, nDs, nMv;
+    uint32_t P;                        /* bytes nLa, nLv, nMv, payload                    */
     uint32_t o0, o1;                   /* outgoing words: body | destination mask << 24   */
     bool wset, wclr;                   /* waitingForReply := 1 / := 0                     */
     bool pendw;                        /* pendingWriteValue := v                          */
     bool asrt;
 };
+
+/* bit-field extract; width 0 gives 0 (v_bfe_u32) */
+DSM_HD uint32_t dt_ubfe(uint32_t x, uint32_t lo, uint32_t w) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_ubfe(x, lo, w);
+#else
+    return w ? ((x >> lo) & ((1u << w) - 1u)) : 0u;
+#endif
+}
 
 DSM_HD uint32_t dt_index(const DtIn &in, uint32_t *evDb_out, uint32_t *own_out) {
     const uint32_t H = in.a >> 4;
@@ -313,10 +323,9 @@ DSM_HD uint32_t dt_index(const DtIn &in, uint32_t *evDb_out, uint32_t *own_out) 
     const uint32_t C = x | (hit << 1) | (in.Ls << 2) | (home << 4) | ((uint32_t)(in.node == in.r2) << 5) |
                        ((uint32_t)(own != in.s) << 6) | (in.Ds << 7) | (((in.Db >> in.s) & 1u) << 9) |
                        ((uint32_t)(rem == 0) << 10) | ((uint32_t)(rem == 1) << 11);
-    const uint32_t cls = (opx < 10) ? ((DT_KCLS0 >> (3 * opx)) & 7u)
-                                    : ((DT_KCLS1 >> (3 * (opx - 10))) & 7u);
+    const uint32_t cls = (uint32_t)((((uint64_t)DT_KCLS1 << 30) | DT_KCLS0) >> (3 * opx)) & 7u;
     const uint32_t lo = (DT_KLO >> (4 * cls)) & 15u, w = (DT_KW >> (4 * cls)) & 15u;
-    const uint32_t sub = w ? ((C >> lo) & ((1u << w) - 1u)) : 0u;
+    const uint32_t sub = dt_ubfe(C, lo, w);
     *evDb_out = evDb;
     *own_out = own;
     return opx * DT_STRIDE + sub;
@@ -348,6 +357,7 @@ DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb, u
     const uint32_t X = in.a | (in.v << 8) | (in.La << 16) | (in.Lv << 24);
     const uint32_t Y = in.pend | (in.Mv << 8) | (in.Db << 16) | ((evDb & 0xFFu) << 24);
     const uint32_t P = dt_perm(Y, X, sel);
+    o.P = P;
     o.nLa = P & 0xFFu;
     o.nLv = (P >> 8) & 0xFFu;
     o.nMv = (P >> 16) & 0xFFu;
