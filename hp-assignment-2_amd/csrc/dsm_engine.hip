@@ -98,7 +98,7 @@ DEVI uint32_t set2(uint32_t w, uint32_t i, uint32_t v) {
 }
 
 /* message body: type[0:3] addr[4:10] payload[11:18] r2[19:21] excl[22];
- * ring entry = body | sender << 23; outbox word = body | destination mask << 24
+ * ring entry = body | sender << 24; outbox word = body | destination mask << 24
  * (built by dt_apply, dsm_table.h) */
 
 /* ---- hashing / generator (definitions in DESIGN.md; pinned by tests) ----------------- */
@@ -281,8 +281,9 @@ sim_kernel(const SimArgs *Ap) {
     }
 
     uint32_t wrounds = 0;    /* loop iterations of this wave (uniform) */
+    uint64_t liveb = __ballot(live);
     for (;;) {
-        if (__ballot(live) == 0) break;
+        if (liveb == 0) break;
         ++wrounds;
 
         /* ---- (1) this round's action, from state at the start of the round ---------- */
@@ -340,7 +341,7 @@ sim_kernel(const SimArgs *Ap) {
         const uint32_t mbw = *mbp;
         DtIn in;
         in.op = op; in.a = a; in.v = (w >> 11) & 0xFFu; in.r2 = (w >> 19) & 7u;
-        in.s = (w >> 23) & 7u; in.excl = (w >> 22) & 1u; in.node = node; in.np_mask = NPM;
+        in.s = w >> 24; in.excl = (w >> 22) & 1u; in.node = node; in.np_mask = NPM;
         in.La = get8(nd.caddr, idx); in.Lv = get8(nd.cval, idx); in.Ls = get2(nd.cst, idx);
         in.Db = mbw >> 8; in.Ds = get2(nd.dst, blk); in.Mv = mbw & 0xFFu; in.pend = nd.ctl & 0xFFu;
         uint32_t evDb, own;
@@ -378,7 +379,9 @@ sim_kernel(const SimArgs *Ap) {
 
         /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        reinterpret_cast<uint2 *>(s_out[wv])[lane] = make_uint2(o0, o1);
+        /* the outbox holds ring entries: body | sender << 24 (the masks stay in o0 / o1) */
+        reinterpret_cast<uint2 *>(s_out[wv])[lane] =
+            make_uint2((o0 & 0xFFFFFFu) | (node << 24), (o1 & 0xFFFFFFu) | (node << 24));
         /* receive masks, transposed at the sender: word j of this node sets bit 2*node + j of
          * every destination's mask (LDS atomic OR; a multicast INV visits its destinations in
          * a short loop), so a receiver reads its mask instead of gathering bits from the
@@ -394,22 +397,22 @@ sim_kernel(const SimArgs *Ap) {
         uint32_t R = s_rm[wv][lane];     /* bit 2*sender+word: that word is addressed to me */
         s_rm[wv][lane] = 0;
         {
-            const uint32_t hh = nd.rh & 0xFFu;
-            uint32_t cc = nd.rh >> 8;
+            /* appended at the tail in R's bit order.  An overflowing ring sets C_OVF and its
+             * tail wraps onto live entries: the system ends this round (the transition
+             * kernel hands it to the 256-deep re-run, which reports RING_OVERFLOW), and the
+             * ring is not part of any record or result. */
+            const uint32_t hh = nd.rh & 0xFFu, cc = nd.rh >> 8;
+            const uint32_t ncc = cc + __builtin_popcount(R);
+            if (ncc > (uint32_t)RING) nd.ctl |= C_OVF;
+            uint32_t slot = hh + cc;
+            slot = slot >= (uint32_t)RING ? slot - RING : slot;
             while (R) {
                 const uint32_t j = __builtin_ctz(R);
                 R &= R - 1;
-                const uint32_t x = s_out[wv][2 * gbase + j];
-                if (cc < (uint32_t)RING) {
-                    const uint32_t slot = hh + cc;
-                    s_ring[wv][slot >= (uint32_t)RING ? slot - RING : slot][lane] =
-                        (x & 0x7FFFFFu) | ((j >> 1) << 23);
-                    ++cc;
-                } else {
-                    nd.ctl |= C_OVF;
-                }
+                s_ring[wv][slot][lane] = s_out[wv][2 * gbase + j];
+                slot = (slot + 1 == (uint32_t)RING) ? 0u : slot + 1;
             }
-            nd.rh = hh | (cc << 8);
+            nd.rh = hh | ((ncc < (uint32_t)RING ? ncc : (uint32_t)RING) << 8);
             rmsg = s_ring[wv][hh][lane];          /* next round's head, prefetched */
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -419,12 +422,23 @@ sim_kernel(const SimArgs *Ap) {
             nxt[0] = pf.x; nxt[1] = pf.y; nxt[2] = pf.z; nxt[3] = pf.w;
         }
 
-        /* ---- (5) per-system termination (Appendix A step 4) -------------------------- */
+        /* ---- (5) per-system termination (Appendix A step 4) -------------------------- *
+         * A round in which no node of a system acts changes nothing, so every later round
+         * is idle too: the active rounds of a system are a prefix, and `rounds` counts every
+         * round, less the final idle one.  The per-round test is wave-uniform: a live group
+         * with no active lane (a zero field in actb | ~liveb), or a lane with an assert, an
+         * overflow or the round limit; the per-lane finish runs only then. */
+        ++rounds;
         const uint64_t actb = __ballot(op != OP_IDLE || stall);    /* stalled = available */
-        const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
+        const uint64_t flagb = __ballot((nd.ctl & (C_ASSERT | C_OVF)) || rounds >= DSM_MAX_ROUNDS);
+        constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
+        constexpr uint64_t GHI = GLO << (NP - 1);
+        const uint64_t t = actb | ~liveb;
+        if ((((t - GLO) & ~t & GHI) | (flagb & liveb)) == 0) continue;
         const uint32_t gact = (uint32_t)(actb >> gbase) & NPM;
+        const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
         const bool gbad = ((badb >> gbase) & NPM) != 0;
-        if (live && gact) ++rounds;
+        if (gact == 0) --rounds;
         const bool done = live && (gact == 0 || gbad || rounds >= DSM_MAX_ROUNDS);
 
         const uint64_t doneb = __ballot(done);
@@ -492,6 +506,7 @@ sim_kernel(const SimArgs *Ap) {
                 else live = false;
             }
         }
+        liveb = __ballot(live);
     }
 
     /* publish this wave's counters */
