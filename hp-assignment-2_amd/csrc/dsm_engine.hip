@@ -97,9 +97,7 @@ DEVI uint32_t set2(uint32_t w, uint32_t i, uint32_t v) {
     return (w & ~(3u << sh)) | (v << sh);
 }
 
-/* message body: type[0:3] addr[4:10] payload[11:18] r2[19:21] excl[22];
- * ring entry = body | sender << 24; outbox word = body | destination mask << 24
- * (built by dt_apply, dsm_table.h) */
+/* message words: dsm_table.h (dt_issue_word, dt_decode, dt_ring_entry) */
 
 /* ---- hashing / generator (definitions in DESIGN.md; pinned by tests) ----------------- */
 DEVI uint64_t fmix64(uint64_t z) {
@@ -324,7 +322,7 @@ sim_kernel(const SimArgs *Ap) {
                 cur[2] = __builtin_amdgcn_alignbit(cur[3], cur[2], 16);
                 cur[3] >>= 16;
             }
-            w = ((ins >> 15) ? OP_WR : OP_RD) | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
+            w = dt_issue_word(ins);                          /* message-word layout */
             if (TR) {                  /* the group's issues of this round, in node order */
                 const uint32_t g = (uint32_t)(__ballot(true) >> gbase) & NPM;
                 const uint32_t pos = nev + __builtin_popcount(g & ((1u << node) - 1u));
@@ -333,15 +331,15 @@ sim_kernel(const SimArgs *Ap) {
             nd.ip++;
         }
         if (TR) nev += __builtin_popcount((uint32_t)(__ballot(doIssue) >> gbase) & NPM);
-        const uint32_t op = (hasMsg || doIssue) ? (w & 15u) : doDump ? OP_DUMP : OP_IDLE;
+        const uint32_t op = (hasMsg || doIssue) ? dt_type(w) : doDump ? OP_DUMP : OP_IDLE;
 
         /* ---- (2) decode, then the micro-op table (dsm_table.h) ------------------------ */
-        const uint32_t a = (w >> 4) & 0x7Fu, blk = a & 15u, idx = a & 3u;  /* :177-184 */
+        DtIn in;
+        dt_decode(w, &in.a, &in.v, &in.excl, &in.r2, &in.s);
+        const uint32_t blk = in.a & 15u, idx = in.a & 3u;                  /* :177-184 */
         uint16_t *const mbp = reinterpret_cast<uint16_t *>(&s_mb[wv][blk >> 1][lane]) + (blk & 1u);
         const uint32_t mbw = *mbp;
-        DtIn in;
-        in.op = op; in.a = a; in.v = (w >> 11) & 0xFFu; in.r2 = (w >> 19) & 7u;
-        in.s = w >> 24; in.excl = (w >> 22) & 1u; in.node = node; in.np_mask = NPM;
+        in.op = op; in.node = node; in.np_mask = NPM;
         in.La = get8(nd.caddr, idx); in.Lv = get8(nd.cval, idx); in.Ls = get2(nd.cst, idx);
         in.Db = mbw >> 8; in.Ds = get2(nd.dst, blk); in.Mv = mbw & 0xFFu; in.pend = nd.ctl & 0xFFu;
         uint32_t evDb, own;
@@ -380,8 +378,7 @@ sim_kernel(const SimArgs *Ap) {
         /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         /* the outbox holds ring entries: body | sender << 24 (the masks stay in o0 / o1) */
-        reinterpret_cast<uint2 *>(s_out[wv])[lane] =
-            make_uint2((o0 & 0xFFFFFFu) | (node << 24), (o1 & 0xFFFFFFu) | (node << 24));
+        reinterpret_cast<uint2 *>(s_out[wv])[lane] = make_uint2(dt_ring_entry(o0, node), dt_ring_entry(o1, node));
         /* receive masks, transposed at the sender: word j of this node sets bit 2*node + j of
          * every destination's mask (LDS atomic OR; a multicast INV visits its destinations in
          * a short loop), so a receiver reads its mask instead of gathering bits from the

@@ -7,7 +7,8 @@
  *
  *   condition vector C (12 bits, per lane):
  *     bit 0 x     = REPLY_RD exclusive flag (msg.bitVector == 2, :245) for REPLY_RD,
- *                   msg.sender == home (:526) for EVICT_SHARED at a non-home node
+ *                   msg.sender == home (:526) for EVICT_SHARED at a non-home node,
+ *                   the WR flag of an issued instruction (RD and WR are one op', DT_RD)
  *     bit 1 hit   = line->address == msg.address
  *     bits 2-3    = line->state (M=0 E=1 S=2 I=3)
  *     bit 4 home  = threadId == procNodeAddr (:182)
@@ -53,12 +54,11 @@ enum : uint32_t { DT_DEM = 0, DT_DS = 1, DT_DU = 2 };             /* directoryEn
 /* classes: 0 none, 1 A [hit Ls], 2 B [x hit Ls], 3 C [hit Ls home atR2], 4 D [fwd Ds],
  *          5 E [Ds sSet rem0 rem1] */
 #define DT_CLS(op) ((op) == DT_RREQ || (op) == DT_WREQ ? 4u :                              \
-                    (op) == DT_RRD || (op) == DT_EVS ? 2u :                                \
+                    (op) == DT_RRD || (op) == DT_EVS || (op) == DT_RD ? 2u :               \
                     (op) == DT_FLUSH || (op) == DT_FLINV ? 3u :                            \
                     (op) == DT_UPG || (op) == DT_EVM || (op) == DT_EVSH ? 5u :             \
                     ((op) == DT_RWR || (op) == DT_RID || (op) == DT_INV ||                 \
-                     (op) == DT_WBINV || (op) == DT_WBINT || (op) == DT_RD ||              \
-                     (op) == DT_WR) ? 1u : 0u)
+                     (op) == DT_WBINV || (op) == DT_WBINT) ? 1u : 0u)
 #define DT_K(op, base) ((uint32_t)DT_CLS((op) + (base)) << (3 * (op)))
 #define DT_KCLS0 (DT_K(0,0) | DT_K(1,0) | DT_K(2,0) | DT_K(3,0) | DT_K(4,0) | DT_K(5,0) |     \
                   DT_K(6,0) | DT_K(7,0) | DT_K(8,0) | DT_K(9,0))
@@ -121,7 +121,7 @@ static inline void dt_entry(uint32_t opx, uint32_t sub, uint32_t *lo_out, uint32
     const uint32_t Ls = (C >> 2) & 3u, Ds = (C >> 7) & 3u;
     const int valid = Ls != DT_CI, hitv = hit && valid;
     uint32_t e = 0, h = 0;
-    switch (opx) {
+    switch ((opx == DT_RD && x) ? DT_WR : opx) {
     case DT_RREQ:                                                     /* :188-236 */
         if (Ds == DT_DU) e = DB_SBIT | E_DS | E_DSV(DT_DEM) | E_O0 | E_O0T(DT_RRD) | E_O0P(1) | E_O0X | E_O0D(0);
         else if (Ds == DT_DS) e = E_DBORS | E_O0 | E_O0T(DT_RRD) | E_O0P(1) | E_O0D(0);
@@ -219,7 +219,6 @@ static inline void dt_entry(uint32_t opx, uint32_t sub, uint32_t *lo_out, uint32
     default:                                                          /* DUMP, IDLE */
         break;
     }
-    (void)x;
     *lo_out = e;
     *hi_out = h;
 }
@@ -237,14 +236,18 @@ enum : uint32_t {
 #define W1_ORS (1u << 2)                   /* | 1 << sender                                  */
 #define W1_ORR (1u << 3)                   /* | 1 << secondReceiver                          */
 #define W1_LS (1u << 4)                    /* line.state = LSV (bits 5-6)                    */
-#define W1_DS (1u << 7)                    /* dir state = DSV (bits 8-9)                     */
-#define W1_O0 (1u << 10)                   /* first word: type bits 11-14                    */
-#define W1_O0LA (1u << 15)                 /*   address = line.address (victim), else a      */
-#define W1_R2(x) ((uint32_t)(x) << 16)     /*   r2 field: 0 zero, 1 sender, 2 secondReceiver */
-#define W1_X (1u << 18)                    /*   exclusive flag                               */
-#define W1_DEST(x) ((uint32_t)(x) << 19)   /*   destination code (E_O0D)                     */
-#define W1_O1(x) ((uint32_t)(x) << 22)     /* second word: 0 none, 1 RREQ, 2 WREQ, 3 UPGRADE  */
-#define W1_O1V (1u << 24)                  /*   payload v                                    */
+#define W1_DS (1u << 7)                    /* dir state = DSV (bits 10-11)                   */
+#define W1_O0 (1u << 8)                    /* first word                                     */
+#define W1_O0LA (1u << 9)                  /*   address = line.address (victim), else a;
+                                            *   bit 9 of a byte-permute selector: byte 2 (La)
+                                            *   instead of byte 0 (a)                         */
+#define W1_R2S (1u << 12)                  /*   secondReceiver field = sender                */
+#define W1_R2R (1u << 13)                  /*   secondReceiver field = secondReceiver        */
+#define W1_O1V (1u << 14)                  /* second word's payload is v                     */
+#define W1_X (1u << 15)                    /*   exclusive flag  } at their places in the     */
+#define W1_T(t) ((uint32_t)(t) << 16)      /*   type (4 bits)   } message word               */
+#define W1_DEST(x) ((uint32_t)(x) << 20)   /*   destination code (E_O0D)                     */
+#define W1_O1(x) ((uint32_t)(x) << 23)     /* second word: 0 none, 1 RREQ, 2 WREQ, 3 UPGRADE  */
 #define W1_WSET (1u << 25)
 #define W1_WCLR (1u << 26)
 #define W1_PEND (1u << 27)
@@ -262,9 +265,9 @@ static inline void dt_compile(uint32_t e, uint32_t h, uint32_t *w0, uint32_t *w1
     *w1 = W1_DBASE((e & E_DBANDS) ? 1u : (e & E_DBAND0) ? 2u : 0u) |
           ((e & E_DBORS) ? W1_ORS : 0u) | ((e & E_DBORR) ? W1_ORR : 0u) |
           ((e & E_LS) ? W1_LS : 0u) | (((e >> 4) & 3u) << 5) |
-          ((e & E_DS) ? W1_DS : 0u) | (((e >> 11) & 3u) << 8) |
-          ((e & E_O0) ? W1_O0 : 0u) | (((e >> 15) & 15u) << 11) | ((e & E_O0LA) ? W1_O0LA : 0u) |
-          W1_R2((e & E_O0RS) ? 1u : (e & E_O0RR) ? 2u : 0u) | ((e & E_O0X) ? W1_X : 0u) |
+          ((e & E_DS) ? W1_DS : 0u) | (((e >> 11) & 3u) << 10) |
+          ((e & E_O0) ? W1_O0 : 0u) | W1_T((e >> 15) & 15u) | ((e & E_O0LA) ? W1_O0LA : 0u) |
+          ((e & E_O0RS) ? W1_R2S : 0u) | ((e & E_O0RR) ? W1_R2R : 0u) | ((e & E_O0X) ? W1_X : 0u) |
           W1_DEST((e >> 25) & 7u) | W1_O1(o1) | ((e & E_O1V) ? W1_O1V : 0u) |
           ((h & E_WSET) ? W1_WSET : 0u) | ((h & E_WCLR) ? W1_WCLR : 0u) |
           ((e & E_PEND) ? W1_PEND : 0u) | ((h & E_ASSERT) ? W1_ASSERT : 0u) |
@@ -283,7 +286,7 @@ static inline void dt_build(uint32_t *tab) {
 
 /* ---- the datapath (host + device) ----------------------------------------------------- */
 struct DtIn {
-    uint32_t op;          /* message type 0..12, DT_RD, DT_WR, DT_DUMP or DT_IDLE           */
+    uint32_t op;          /* message type 0..12, DT_RD (an issued RD or WR), DT_DUMP, DT_IDLE */
     uint32_t a, v, r2, s, excl;        /* decoded message / instruction word             */
     uint32_t node, np_mask;
     uint32_t La, Lv, Ls;               /* line at a % 4                                   */
@@ -298,6 +301,21 @@ struct DtOut {
     bool pendw;                        /* pendingWriteValue := v                          */
     bool asrt;
 };
+
+/* ---- message words ---------------------------------------------------------------------
+ * A message word (ring entry, outbox word) is laid out like an issued instruction:
+ *   bits 0-7 payload (value), 8-14 address, 15 exclusive flag (REPLY_RD) or the WR flag of
+ *   an instruction, 16-19 type, 20-22 secondReceiver, 24-31 sender (ring entry) or
+ *   destination mask (outbox word).
+ * So an instruction of the packed trace (WR << 15 | address << 8 | value, DSM_PACK_INSTR)
+ * becomes a word of type DT_RD by one OR, and the first outgoing word's payload and
+ * address bytes come out of one byte permute.                                             */
+DSM_HD uint32_t dt_issue_word(uint32_t ins) { return ins | (DT_RD << 16); }
+DSM_HD uint32_t dt_type(uint32_t w) { return (w >> 16) & 15u; }
+DSM_HD uint32_t dt_ring_entry(uint32_t o, uint32_t sender) { return (o & 0xFFFFFFu) | (sender << 24); }
+DSM_HD void dt_decode(uint32_t w, uint32_t *a, uint32_t *v, uint32_t *excl, uint32_t *r2, uint32_t *s) {
+    *a = (w >> 8) & 0x7Fu; *v = w & 0xFFu; *excl = (w >> 15) & 1u; *r2 = (w >> 20) & 7u; *s = (w >> 24) & 7u;
+}
 
 /* bit-field extract; width 0 gives 0 (v_bfe_u32) */
 DSM_HD uint32_t dt_ubfe(uint32_t x, uint32_t lo, uint32_t w) {
@@ -318,7 +336,7 @@ DSM_HD uint32_t dt_index(const DtIn &in, uint32_t *evDb_out, uint32_t *own_out) 
     const uint32_t rem = (uint32_t)__builtin_popcount(evDb & in.np_mask);    /* countSharers */
     uint32_t opx = in.op;
     opx = (opx == DT_EVS && home) ? DT_EVSH : opx;
-    opx = ((opx == DT_RD || opx == DT_WR) && !((in.np_mask >> H) & 1u)) ? DT_ASSERT : opx;  /* :602 */
+    opx = (opx == DT_RD && !((in.np_mask >> H) & 1u)) ? DT_ASSERT : opx;                    /* :602 */
     const uint32_t x = (in.op == DT_EVS) ? (uint32_t)(in.s == H) : in.excl;
     const uint32_t C = x | (hit << 1) | (in.Ls << 2) | (home << 4) | ((uint32_t)(in.node == in.r2) << 5) |
                        ((uint32_t)(own != in.s) << 6) | (in.Ds << 7) | (((in.Db >> in.s) & 1u) << 9) |
@@ -361,29 +379,28 @@ DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb, u
     o.nLa = P & 0xFFu;
     o.nLv = (P >> 8) & 0xFFu;
     o.nMv = (P >> 16) & 0xFFu;
-    const uint32_t pay = P >> 24;
     /* cache line state, directory entry */
     o.nLs = (lineOn && (W1 & W1_LS)) ? ((W1 >> 5) & 3u) : in.Ls;
     const uint32_t db = W1 & 3u;
     const uint32_t base = (db & 2u) ? 0u : (db ? (evDb & 0xFFu) : in.Db);
     o.nDb = base | ((W1 & W1_ORS) ? sbit : 0u) | ((W1 & W1_ORR) ? (1u << in.r2) : 0u);
-    o.nDs = (W1 & W1_DS) ? ((W1 >> 8) & 3u) : in.Ds;
-    /* first outgoing word */
-    const uint32_t rc = (W1 >> 16) & 3u;
-    const uint32_t r2f = (rc & 2u) ? in.r2 : (rc ? in.s : 0u);
-    const uint32_t dc = (W1 >> 19) & 7u;
+    o.nDs = (W1 & W1_DS) ? ((W1 >> 10) & 3u) : in.Ds;
+    /* first outgoing word: payload and address bytes by one permute of {P, X} (payload =
+     * P byte 3; address = X byte 0 (a) or byte 2 (La), per W1_O0LA at selector bit 9),
+     * exclusive flag and type straight from W1, secondReceiver field, destinations */
+    const uint32_t lo16 = dt_perm(P, X, 0x0C0C0007u | (W1 & W1_O0LA));
+    const uint32_t r2f = ((W1 & W1_R2S) ? in.s : 0u) | ((W1 & W1_R2R) ? in.r2 : 0u);
+    const uint32_t dc = (W1 >> 20) & 7u;
     const bool d0 = dc & 1u, d1 = dc & 2u, d2 = dc & 4u;
     const uint32_t ctzEv = (uint32_t)__builtin_ctz((evDb & in.np_mask) | 0x80000000u);
     const uint32_t didx = d1 ? (d0 ? ctzEv : (in.La >> 4)) : (d0 ? own : in.s);
     const uint32_t mset = d0 ? (in.v & in.np_mask & ~(1u << in.node)) : ((1u << H) | (1u << in.r2));
     const uint32_t dm = d2 ? mset : (1u << didx);
     const bool on0 = (W1 & W1_O0) && (!(W1 & W1_O0NFF) || !laFF);
-    const uint32_t addr0 = (W1 & W1_O0LA) ? in.La : in.a;
-    o.o0 = on0 ? (((W1 >> 11) & 15u) | (addr0 << 4) | (pay << 11) | (r2f << 19) |
-                  (((W1 >> 18) & 1u) << 22) | (dm << 24)) : 0u;
+    o.o0 = on0 ? (lo16 | (W1 & (W1_X | W1_T(15))) | (r2f << 20) | (dm << 24)) : 0u;
     /* second outgoing word: the request to the home (type RREQ 0 / WREQ 1 / UPGRADE 6) */
-    const uint32_t c1 = (W1 >> 22) & 3u;
-    o.o1 = c1 ? (((0x6100u >> (4 * c1)) & 15u) | (in.a << 4) | (((W1 & W1_O1V) ? in.v : 0u) << 11) |
+    const uint32_t c1 = (W1 >> 23) & 3u;
+    o.o1 = c1 ? ((((0x6100u >> (4 * c1)) & 15u) << 16) | (in.a << 8) | ((W1 & W1_O1V) ? in.v : 0u) |
                  (1u << (24 + H))) : 0u;
     o.wset = lineOn && (W1 & W1_WSET);
     o.wclr = lineOn && (W1 & W1_WCLR);

@@ -58,7 +58,7 @@ int run_one(Sys &y, const uint32_t *tab, const Src &src, dsm_res *res) {
                 w = y.ring[me][y.head[me]];
                 y.head[me] = (y.head[me] + 1) % 256;
                 y.cnt[me]--;
-                op = w & 15u;
+                op = dt_type(w);
                 ++msgs;
             } else if (s.flags & 1) {
                 op = DT_IDLE;
@@ -66,8 +66,8 @@ int run_one(Sys &y, const uint32_t *tab, const Src &src, dsm_res *res) {
                 const uint32_t ins = src.at(np, me, s.issued);
                 s.issued++;
                 ++instrs;
-                w = ((ins >> 15) ? DT_WR : DT_RD) | (((ins >> 8) & 0x7Fu) << 4) | ((ins & 0xFFu) << 11);
-                op = w & 15u;
+                w = dt_issue_word(ins);
+                op = dt_type(w);
             } else if (!(s.flags & 2)) {
                 op = DT_DUMP;
                 s.flags |= 2;
@@ -76,10 +76,10 @@ int run_one(Sys &y, const uint32_t *tab, const Src &src, dsm_res *res) {
                 op = DT_IDLE;
             }
             if (op != DT_IDLE) acted = 1;
-            const uint32_t a = (w >> 4) & 0x7Fu, blk = a & 15u, idx = a & 3u;
             DtIn in;
-            in.op = op; in.a = a; in.v = (w >> 11) & 0xFFu; in.r2 = (w >> 19) & 7u;
-            in.s = (w >> 23) & 7u; in.excl = (w >> 22) & 1u; in.node = (uint32_t)me; in.np_mask = npm;
+            dt_decode(w, &in.a, &in.v, &in.excl, &in.r2, &in.s);
+            const uint32_t blk = in.a & 15u, idx = in.a & 3u;
+            in.op = op; in.node = (uint32_t)me; in.np_mask = npm;
             in.La = s.cache_addr[idx]; in.Lv = s.cache_value[idx]; in.Ls = s.cache_state[idx];
             in.Db = s.dir_bv[blk]; in.Ds = s.dir_state[blk]; in.Mv = s.memory[blk]; in.pend = s.pending;
             uint32_t evDb, own;
@@ -103,7 +103,7 @@ int run_one(Sys &y, const uint32_t *tab, const Src &src, dsm_res *res) {
                 for (int d = 0; d < np; ++d)
                     if ((x >> (24 + d)) & 1u) {
                         if (y.cnt[d] >= y.cap) { ovf = 1; break; }
-                        y.ring[d][(y.head[d] + y.cnt[d]) % 256] = (x & 0x7FFFFFu) | ((uint32_t)sd << 23);
+                        y.ring[d][(y.head[d] + y.cnt[d]) % 256] = dt_ring_entry(x, (uint32_t)sd);
                         y.cnt[d]++;
                     }
             }
