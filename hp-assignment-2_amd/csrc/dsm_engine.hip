@@ -80,7 +80,7 @@ enum : uint32_t {
 };
 
 /* ctl word: bits 0-7 pendingWriteValue, then flags */
-constexpr uint32_t C_WAIT = 1u << 8, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C_ASSERT = 1u << 11;
+constexpr uint32_t C_WAIT = DT_CTL_WAIT, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C_ASSERT = DT_CTL_ASSERT;
 
 /* counter slots (dsm_counters order) */
 enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
@@ -357,12 +357,7 @@ sim_kernel(const SimArgs *Ap) {
         nd.cst = set2(nd.cst, idx, o.nLs);
         nd.dst = set2(nd.dst, blk, o.nDs);
         *mbp = (uint16_t)(o.nMv | (o.nDb << 8));
-        uint32_t ctl = nd.ctl;
-        ctl = o.wclr ? (ctl & ~C_WAIT) : ctl;
-        ctl = o.wset ? (ctl | C_WAIT) : ctl;
-        ctl = o.pendw ? ((ctl & ~0xFFu) | in.v) : ctl;                   /* :633 */
-        ctl = o.asrt ? (ctl | C_ASSERT) : ctl;
-        nd.ctl = ctl;
+        nd.ctl = (nd.ctl & ~o.cclr) | o.cset;      /* wait, pendingWriteValue (:633), assert */
         const bool isMsg = op <= T_EVM;
         nd.nmsg += isMsg ? 1u : 0u;
         if (TC) {

@@ -232,46 +232,53 @@ enum : uint32_t {
     DP_A = 0, DP_V = 1, DP_LA = 2, DP_LV = 3, DP_PEND = 4, DP_MV = 5, DP_DB = 6, DP_EVDB = 7,
     DP_ZERO = 12
 };
-#define W1_DBASE(x) ((uint32_t)(x) << 0)   /* dir bv base: 0 bv, 1 bv & ~sbit, 2 zero        */
-#define W1_ORS (1u << 2)                   /* | 1 << sender                                  */
-#define W1_ORR (1u << 3)                   /* | 1 << secondReceiver                          */
-#define W1_LS (1u << 4)                    /* line.state = LSV (bits 5-6)                    */
-#define W1_DS (1u << 7)                    /* dir state = DSV (bits 10-11)                   */
-#define W1_O0 (1u << 8)                    /* first word                                     */
+#define W1_LSEL(x) ((uint32_t)(x) << 0)    /* line.state: selector 0 keep, 4 + k state k     */
+#define W1_ORS (1u << 3)                   /* dir bv |= 1 << sender                          */
+#define W1_ORR (1u << 4)                   /* dir bv |= 1 << secondReceiver                  */
+#define W1_DBASE(x) ((uint32_t)(x) << 5)   /* dir bv base: 0 bv, 1 bv & ~sbit, 2 zero        */
+#define W1_O0 (1u << 7)                    /* first word                                     */
+#define W1_O1V (1u << 8)                   /* second word's payload is v                     */
 #define W1_O0LA (1u << 9)                  /*   address = line.address (victim), else a;
                                             *   bit 9 of a byte-permute selector: byte 2 (La)
                                             *   instead of byte 0 (a)                         */
-#define W1_R2S (1u << 12)                  /*   secondReceiver field = sender                */
-#define W1_R2R (1u << 13)                  /*   secondReceiver field = secondReceiver        */
-#define W1_O1V (1u << 14)                  /* second word's payload is v                     */
+#define W1_DEST(x) ((uint32_t)(x) << 10)   /*   destination code (E_O0D)                     */
+#define W1_R2S (1u << 13)                  /*   secondReceiver field = sender                */
+#define W1_R2R (1u << 14)                  /*   secondReceiver field = secondReceiver        */
 #define W1_X (1u << 15)                    /*   exclusive flag  } at their places in the     */
 #define W1_T(t) ((uint32_t)(t) << 16)      /*   type (4 bits)   } message word               */
-#define W1_DEST(x) ((uint32_t)(x) << 20)   /*   destination code (E_O0D)                     */
-#define W1_O1(x) ((uint32_t)(x) << 23)     /* second word: 0 none, 1 RREQ, 2 WREQ, 3 UPGRADE  */
-#define W1_WSET (1u << 25)
-#define W1_WCLR (1u << 26)
-#define W1_PEND (1u << 27)
-#define W1_ASSERT (1u << 28)
-#define W1_O0NFF (1u << 29)                /* first word only if line.address != 0xFF        */
-#define W1_FFG (1u << 30)                  /* assert only, line/wait effects only, if line.address == 0xFF resp. not */
+#define W1_WSET (1u << 20)
+#define W1_WCLR (1u << 21)
+#define W1_PEND (1u << 22)
+#define W1_ASSERT (1u << 23)
+#define W1_DSEL(x) ((uint32_t)(x) << 24)   /* dir state: selector 1 keep, 4 + k state k      */
+#define W1_O1(x) ((uint32_t)(x) << 27)     /* second word: 0 none, 1 RREQ, 2 WREQ, 3 UPGRADE  */
 
+/* The 0xFF gates of dt_entry are resolved here.  A line leaves INVALID only by being filled
+ * (line.address = a <= 0x7F), and line.address never returns to 0xFF, so a valid line never
+ * has address 0xFF: the victim word (handleCacheReplacement :742-745 skips INVALID and 0xFF)
+ * is only ever emitted for a valid line, and the REPLY_WR / FLUSH_INVACK asserts (:443,
+ * :489), which the table raises only for a valid non-matching line, always fire there,
+ * before any line or wait update.  (tests/model/table_model.cpp checks the invariant.)  */
 static inline void dt_compile(uint32_t e, uint32_t h, uint32_t *w0, uint32_t *w1) {
     static const uint32_t lv_sel[4] = {DP_LV, DP_V, DP_PEND, DP_ZERO};    /* E_LV codes  */
     static const uint32_t pay_sel[4] = {DP_ZERO, DP_MV, DP_EVDB, DP_LV};  /* E_O0P codes */
+    if (h & E_LINEFF) {                                /* the assert fires: no line effects */
+        e &= ~(E_LA | E_LV(3) | E_LS | E_LSV(3));
+        h &= ~(E_WSET | E_WCLR);
+    }
     *w0 = ((e & E_LA) ? DP_A : DP_LA) | (lv_sel[(e >> 1) & 3u] << 8) |
           (((e & E_MEM) ? DP_V : DP_MV) << 16) | (pay_sel[(e >> 20) & 3u] << 24);
     const uint32_t t1 = (h >> 8) & 15u;
     const uint32_t o1 = !(e & E_O1) ? 0u : t1 == DT_RREQ ? 1u : t1 == DT_WREQ ? 2u : 3u;
-    *w1 = W1_DBASE((e & E_DBANDS) ? 1u : (e & E_DBAND0) ? 2u : 0u) |
+    *w1 = W1_LSEL((e & E_LS) ? 4u + ((e >> 4) & 3u) : 0u) |
+          W1_DSEL((e & E_DS) ? 4u + ((e >> 11) & 3u) : 1u) |
+          W1_DBASE((e & E_DBANDS) ? 1u : (e & E_DBAND0) ? 2u : 0u) |
           ((e & E_DBORS) ? W1_ORS : 0u) | ((e & E_DBORR) ? W1_ORR : 0u) |
-          ((e & E_LS) ? W1_LS : 0u) | (((e >> 4) & 3u) << 5) |
-          ((e & E_DS) ? W1_DS : 0u) | (((e >> 11) & 3u) << 10) |
           ((e & E_O0) ? W1_O0 : 0u) | W1_T((e >> 15) & 15u) | ((e & E_O0LA) ? W1_O0LA : 0u) |
           ((e & E_O0RS) ? W1_R2S : 0u) | ((e & E_O0RR) ? W1_R2R : 0u) | ((e & E_O0X) ? W1_X : 0u) |
           W1_DEST((e >> 25) & 7u) | W1_O1(o1) | ((e & E_O1V) ? W1_O1V : 0u) |
           ((h & E_WSET) ? W1_WSET : 0u) | ((h & E_WCLR) ? W1_WCLR : 0u) |
-          ((e & E_PEND) ? W1_PEND : 0u) | ((h & E_ASSERT) ? W1_ASSERT : 0u) |
-          ((h & E_O0NFF) ? W1_O0NFF : 0u) | ((h & (E_ANFF | E_LINEFF)) ? W1_FFG : 0u);
+          ((e & E_PEND) ? W1_PEND : 0u) | ((h & E_ASSERT) ? W1_ASSERT : 0u);
 }
 
 /* the whole table, compiled: tab[2 * i] = W0, tab[2 * i + 1] = W1 */
@@ -300,7 +307,12 @@ struct DtOut {
     bool wset, wclr;                   /* waitingForReply := 1 / := 0                     */
     bool pendw;                        /* pendingWriteValue := v                          */
     bool asrt;
+    uint32_t cset, cclr;               /* the same as a control-word update               */
 };
+/* node control word bits touched by cset / cclr (dsm_engine.hip's C_WAIT, C_ASSERT) */
+enum : uint32_t { DT_CTL_WAIT = 1u << 8, DT_CTL_ASSERT = 1u << 11 };
+static_assert((W1_WSET >> 12) == DT_CTL_WAIT && (W1_ASSERT >> 12) == DT_CTL_ASSERT &&
+              (W1_WCLR >> 13) == DT_CTL_WAIT, "W1 control bits");
 
 /* ---- message words ---------------------------------------------------------------------
  * A message word (ring entry, outbox word) is laid out like an issued instruction:
@@ -368,44 +380,45 @@ DSM_HD uint32_t dt_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
 DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb, uint32_t own) {
     DtOut o;
     const uint32_t H = in.a >> 4, sbit = 1u << in.s;
-    const bool laFF = (in.La == 0xFFu);
-    const bool lineOn = !(W1 & W1_FFG) || laFF;
-    /* the four byte outputs in one byte permute; line effects off = keep La, Lv */
-    const uint32_t sel = lineOn ? W0 : ((W0 & 0xFFFF0000u) | (DP_LV << 8) | DP_LA);
+    /* the four byte results in one byte permute */
     const uint32_t X = in.a | (in.v << 8) | (in.La << 16) | (in.Lv << 24);
     const uint32_t Y = in.pend | (in.Mv << 8) | (in.Db << 16) | ((evDb & 0xFFu) << 24);
-    const uint32_t P = dt_perm(Y, X, sel);
+    const uint32_t P = dt_perm(Y, X, W0);
     o.P = P;
     o.nLa = P & 0xFFu;
     o.nLv = (P >> 8) & 0xFFu;
     o.nMv = (P >> 16) & 0xFFu;
-    /* cache line state, directory entry */
-    o.nLs = (lineOn && (W1 & W1_LS)) ? ((W1 >> 5) & 3u) : in.Ls;
-    const uint32_t db = W1 & 3u;
+    /* line and directory states: a permute of {Ls, Ds} and the constants 0..3 */
+    const uint32_t S = dt_perm(0x03020100u, in.Ls | (in.Ds << 8), W1 & (W1_LSEL(7) | W1_DSEL(7)));
+    o.nLs = S & 0xFFu;
+    o.nDs = S >> 24;
+    const uint32_t db = (W1 >> 5) & 3u;
     const uint32_t base = (db & 2u) ? 0u : (db ? (evDb & 0xFFu) : in.Db);
     o.nDb = base | ((W1 & W1_ORS) ? sbit : 0u) | ((W1 & W1_ORR) ? (1u << in.r2) : 0u);
-    o.nDs = (W1 & W1_DS) ? ((W1 >> 10) & 3u) : in.Ds;
     /* first outgoing word: payload and address bytes by one permute of {P, X} (payload =
      * P byte 3; address = X byte 0 (a) or byte 2 (La), per W1_O0LA at selector bit 9),
      * exclusive flag and type straight from W1, secondReceiver field, destinations */
     const uint32_t lo16 = dt_perm(P, X, 0x0C0C0007u | (W1 & W1_O0LA));
     const uint32_t r2f = ((W1 & W1_R2S) ? in.s : 0u) | ((W1 & W1_R2R) ? in.r2 : 0u);
-    const uint32_t dc = (W1 >> 20) & 7u;
+    const uint32_t dc = (W1 >> 10) & 7u;
     const bool d0 = dc & 1u, d1 = dc & 2u, d2 = dc & 4u;
     const uint32_t ctzEv = (uint32_t)__builtin_ctz((evDb & in.np_mask) | 0x80000000u);
     const uint32_t didx = d1 ? (d0 ? ctzEv : (in.La >> 4)) : (d0 ? own : in.s);
     const uint32_t mset = d0 ? (in.v & in.np_mask & ~(1u << in.node)) : ((1u << H) | (1u << in.r2));
     const uint32_t dm = d2 ? mset : (1u << didx);
-    const bool on0 = (W1 & W1_O0) && (!(W1 & W1_O0NFF) || !laFF);
-    o.o0 = on0 ? (lo16 | (W1 & (W1_X | W1_T(15))) | (r2f << 20) | (dm << 24)) : 0u;
+    o.o0 = (W1 & W1_O0) ? (lo16 | (W1 & (W1_X | W1_T(15))) | (r2f << 20) | (dm << 24)) : 0u;
     /* second outgoing word: the request to the home (type RREQ 0 / WREQ 1 / UPGRADE 6) */
-    const uint32_t c1 = (W1 >> 23) & 3u;
+    const uint32_t c1 = (W1 >> 27) & 3u;
     o.o1 = c1 ? ((((0x6100u >> (4 * c1)) & 15u) << 16) | (in.a << 8) | ((W1 & W1_O1V) ? in.v : 0u) |
                  (1u << (24 + H))) : 0u;
-    o.wset = lineOn && (W1 & W1_WSET);
-    o.wclr = lineOn && (W1 & W1_WCLR);
+    /* node control word (pending byte, wait bit 8, assert bit 11): ctl' = ctl & ~cclr | cset */
+    const uint32_t pm = (W1 & W1_PEND) ? 0xFFu : 0u;
+    o.cset = ((W1 >> 12) & (DT_CTL_WAIT | DT_CTL_ASSERT)) | (in.v & pm);   /* WSET, ASSERT */
+    o.cclr = ((W1 >> 13) & DT_CTL_WAIT) | pm;                                /* WCLR        */
+    o.wset = (W1 & W1_WSET) != 0u;
+    o.wclr = (W1 & W1_WCLR) != 0u;
     o.pendw = (W1 & W1_PEND) != 0u;
-    o.asrt = (W1 & W1_ASSERT) && (!(W1 & W1_FFG) || !laFF);
+    o.asrt = (W1 & W1_ASSERT) != 0u;
     return o;
 }
 

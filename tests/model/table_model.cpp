@@ -87,6 +87,10 @@ int run_one(Sys &y, const uint32_t *tab, const Src &src, dsm_res *res) {
             const DtOut o = dt_apply(in, tab[2 * ti], tab[2 * ti + 1], evDb, own);
             s.cache_addr[idx] = (uint8_t)o.nLa; s.cache_value[idx] = (uint8_t)o.nLv;
             s.cache_state[idx] = (uint8_t)o.nLs;
+            if (o.nLs != DT_CI && o.nLa == 0xFFu) {     /* the invariant dt_compile relies on */
+                fprintf(stderr, "valid line with address 0xFF\n");
+                abort();
+            }
             s.dir_bv[blk] = (uint8_t)o.nDb; s.dir_state[blk] = (uint8_t)o.nDs;
             s.memory[blk] = (uint8_t)o.nMv;
             if (o.wset) s.flags |= 1;
