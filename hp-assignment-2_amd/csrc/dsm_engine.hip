@@ -213,13 +213,13 @@ sim_kernel(const SimArgs *Ap) {
     __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][128]; /* 2 words/lane  */
     __shared__ uint32_t s_rm[WAVES][64];                               /* receive masks */
     __shared__ unsigned long long s_cnt[WAVES][K_N];
-    __shared__ uint2 s_tab[DT_ENTRIES];                                /* micro-op table */
+    __shared__ uint2 s_tab[DT_TABLE_WORDS / 2];                /* micro-op table + header */
 
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t node = lane % NP, gbase = lane - node;
     if (lane < K_N) s_cnt[wv][lane] = 0;
     s_rm[wv][lane] = 0;
-    for (uint32_t i = threadIdx.x; i < DT_ENTRIES; i += 64 * WAVES) s_tab[i] = Ap->table[i];
+    for (uint32_t i = threadIdx.x; i < DT_TABLE_WORDS / 2; i += 64 * WAVES) s_tab[i] = Ap->table[i];
     __syncthreads();
 
     const uint64_t n = Ap->d_n ? (uint64_t)*Ap->d_n : Ap->n_sys;
@@ -342,10 +342,12 @@ sim_kernel(const SimArgs *Ap) {
         in.op = op; in.node = node; in.np_mask = NPM;
         in.La = get8(nd.caddr, idx); in.Lv = get8(nd.cval, idx); in.Ls = get2(nd.cst, idx);
         in.Db = mbw >> 8; in.Ds = get2(nd.dst, blk); in.Mv = mbw & 0xFFu; in.pend = nd.ctl & 0xFFu;
-        uint32_t evDb, own;
-        const uint32_t ti = dt_index(in, &evDb, &own);
+        uint32_t evDb;
+        const uint32_t opx = dt_opx(in);
+        const uint32_t hdr = reinterpret_cast<const uint8_t *>(&s_tab[DT_ENTRIES])[opx];
+        const uint32_t ti = dt_index(in, opx, hdr, &evDb);
         const uint2 E = s_tab[ti];
-        const DtOut o = dt_apply(in, E.x, E.y, evDb, own);
+        const DtOut o = dt_apply(in, E.x, E.y, evDb);
         const uint32_t o0 = o.o0, o1 = o.o1;
 
         /* ---- (3) write back (idle lanes rewrite unchanged values) ------------------- */
@@ -682,7 +684,7 @@ sim_fn pick_fallback(int np, bool gen, int mode) {
     return gen ? fb_np_gen<8, true>(mode) : fb_np_gen<8, false>(mode);
 }
 int lds_bytes(int ring, int waves) {
-    return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 4 + K_N * 8) + DT_ENTRIES * 8;
+    return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 4 + K_N * 8) + DT_TABLE_WORDS * 4;
 }
 
 }  // namespace
@@ -734,12 +736,12 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
         hipHostMalloc((void **)&c->h_args, 2 * sizeof(SimArgs), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_args, hipEventDisableTiming) != hipSuccess ||
         hipMalloc((void **)&c->d_cnt, sizeof(dsm_counters)) != hipSuccess ||
-        hipMalloc((void **)&c->d_table, DT_ENTRIES * sizeof(uint2)) != hipSuccess) {
+        hipMalloc((void **)&c->d_table, DT_TABLE_WORDS * sizeof(uint32_t)) != hipSuccess) {
         dsm_close(c);
         return DSM_E_DEVICE;
     }
     {
-        static uint32_t tab[2 * DT_ENTRIES];
+        static uint32_t tab[DT_TABLE_WORDS];
         dt_build(tab);
         if (hipMemcpy(c->d_table, tab, sizeof tab, hipMemcpyHostToDevice) != hipSuccess) {
             dsm_close(c);

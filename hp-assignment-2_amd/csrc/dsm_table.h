@@ -5,22 +5,25 @@
  * model used by the tests).  The 13 message handlers of assignment.c (:177-566) and the
  * instruction issue (:590-687) are compiled into a 640-entry micro-op table:
  *
- *   condition vector C (12 bits, per lane):
- *     bit 0 x     = REPLY_RD exclusive flag (msg.bitVector == 2, :245) for REPLY_RD,
- *                   msg.sender == home (:526) for EVICT_SHARED at a non-home node,
+ *   condition vector C (11 bits, per lane):
+ *     bit 0 x     = the word's exclusive flag: REPLY_RD exclusive (msg.bitVector == 2,
+ *                   :245); for EVICT_SHARED at a non-home node msg.sender == home (:526),
+ *                   which its only sender (the home, EVICT_SHARED handler :515) sets;
  *                   the WR flag of an issued instruction (RD and WR are one op', DT_RD)
  *     bit 1 hit   = line->address == msg.address
  *     bits 2-3    = line->state (M=0 E=1 S=2 I=3)
  *     bit 4 home  = threadId == procNodeAddr (:182)
  *     bit 5 atR2  = threadId == msg.secondReceiver (:286, :483)
- *     bit 6 fwd   = findOwner(dirEntry->bitVector) != msg.sender (:215, :410)
- *     bits 7-8    = dirEntry->state (EM=0 S=1 U=2)
- *     bit 9 sSet  = isBitSet(dirEntry->bitVector, msg.sender) (:501, :545)
- *     bit 10/11   = countSharers after clearing the sender == 0 / == 1 (:504-507)
+ *     bits 6-7    = dirEntry->state (EM=0 S=1 U=2)
+ *     bit 8 sSet  = isBitSet(dirEntry->bitVector, msg.sender) (:501, :545); in state EM the
+ *                   bitVector holds exactly one bit, so findOwner(bv) != msg.sender (:215,
+ *                   :410) is !sSet (tests/model/table_model.cpp checks the invariant)
+ *     bits 9-10   = countSharers after clearing the sender: 0, 1 or 2 = more (:504-507)
  *   op' = the message type / issue op, with EVICT_SHARED at its home as its own op (17)
  *         and an unsimulatable instruction (home >= np) as ASSERT (18);
- *   each op' reads one contiguous bit-field of C (its class: lo, width), so
- *   index = op' * 32 + bfe(C, lo, width) -- no per-op branch anywhere.
+ *   each op' reads one contiguous bit-field of C (its class: lo, width; a byte per op' in
+ *   the table's header, dt_hdr), so index = op' * 32 + bfe(C, lo, width) -- no per-op
+ *   branch anywhere.
  *
  * An entry (64 bits) says what to do with the cache line, the directory entry, the memory
  * byte, the two outgoing message words (templates whose operands are picked from a few
@@ -45,14 +48,15 @@ enum : uint32_t {
     DT_RREQ = 0, DT_WREQ = 1, DT_RRD = 2, DT_RWR = 3, DT_RID = 4, DT_INV = 5, DT_UPG = 6,
     DT_WBINV = 7, DT_WBINT = 8, DT_FLUSH = 9, DT_FLINV = 10, DT_EVS = 11, DT_EVM = 12,
     DT_RD = 13, DT_WR = 14, DT_DUMP = 15, DT_IDLE = 16, DT_EVSH = 17, DT_ASSERT = 18,
-    DT_NOPS = 20, DT_STRIDE = 32, DT_ENTRIES = DT_NOPS * DT_STRIDE
+    DT_NOPS = 20, DT_STRIDE = 32, DT_ENTRIES = DT_NOPS * DT_STRIDE,
+    DT_HDR_WORDS = 8, DT_TABLE_WORDS = 2 * DT_ENTRIES + DT_HDR_WORDS
 };
 enum : uint32_t { DT_CM = 0, DT_CE = 1, DT_CS = 2, DT_CI = 3 };   /* cacheLineState :17 */
 enum : uint32_t { DT_DEM = 0, DT_DS = 1, DT_DU = 2 };             /* directoryEntryState :18 */
 
 /* class of each op' (3 bits each; ops 0-9 in K0, 10-19 in K1) and (lo, width) per class */
-/* classes: 0 none, 1 A [hit Ls], 2 B [x hit Ls], 3 C [hit Ls home atR2], 4 D [fwd Ds],
- *          5 E [Ds sSet rem0 rem1] */
+/* classes: 0 none, 1 A [hit Ls], 2 B [x hit Ls], 3 C [hit Ls home atR2], 4 D [Ds sSet],
+ *          5 E [Ds sSet rem] */
 #define DT_CLS(op) ((op) == DT_RREQ || (op) == DT_WREQ ? 4u :                              \
                     (op) == DT_RRD || (op) == DT_EVS || (op) == DT_RD ? 2u :               \
                     (op) == DT_FLUSH || (op) == DT_FLINV ? 3u :                            \
@@ -64,7 +68,7 @@ enum : uint32_t { DT_DEM = 0, DT_DS = 1, DT_DU = 2 };             /* directoryEn
                   DT_K(6,0) | DT_K(7,0) | DT_K(8,0) | DT_K(9,0))
 #define DT_KCLS1 (DT_K(0,10) | DT_K(1,10) | DT_K(2,10) | DT_K(3,10) | DT_K(4,10) |           \
                   DT_K(5,10) | DT_K(6,10) | DT_K(7,10) | DT_K(8,10) | DT_K(9,10))
-#define DT_KLO 0x761010u   /* nibble per class: lo bit of its field in C  */
+#define DT_KLO 0x661010u   /* nibble per class: lo bit of its field in C  */
 #define DT_KW 0x535430u    /* nibble per class: width of its field        */
 
 /* entry, low word.  Every multi-way choice is encoded as independent bits, so the datapath
@@ -117,8 +121,9 @@ static inline void dt_entry(uint32_t opx, uint32_t sub, uint32_t *lo_out, uint32
     const uint32_t lo = (DT_KLO >> (4 * cls)) & 15u, w = (DT_KW >> (4 * cls)) & 15u;
     const uint32_t C = (w ? (sub & ((1u << w) - 1u)) : 0u) << lo;
     const int x = C & 1, hit = (C >> 1) & 1, home = (C >> 4) & 1, atR2 = (C >> 5) & 1;
-    const int fwd = (C >> 6) & 1, sSet = (C >> 9) & 1, rem0 = (C >> 10) & 1, rem1 = (C >> 11) & 1;
-    const uint32_t Ls = (C >> 2) & 3u, Ds = (C >> 7) & 3u;
+    const int sSet = (C >> 8) & 1, fwd = !sSet;
+    const int rem0 = ((C >> 9) & 3u) == 0, rem1 = ((C >> 9) & 3u) == 1;
+    const uint32_t Ls = (C >> 2) & 3u, Ds = (C >> 6) & 3u;
     const int valid = Ls != DT_CI, hitv = hit && valid;
     uint32_t e = 0, h = 0;
     switch ((opx == DT_RD && x) ? DT_WR : opx) {
@@ -188,7 +193,8 @@ static inline void dt_entry(uint32_t opx, uint32_t sub, uint32_t *lo_out, uint32
         if (sSet) {
             e = E_DBANDS;
             if (rem0) e |= E_DS | E_DSV(DT_DU);
-            else if (rem1 && Ds == DT_DS) e |= E_DS | E_DSV(DT_DEM) | E_O0 | E_O0T(DT_EVS) | E_O0D(3);
+            else if (rem1 && Ds == DT_DS)       /* the EVICT_SHARED comes from the home: x */
+                e |= E_DS | E_DSV(DT_DEM) | E_O0 | E_O0T(DT_EVS) | E_O0X | E_O0D(3);
         }
         break;
     case DT_EVM:                                                      /* :541-561 */
@@ -281,7 +287,8 @@ static inline void dt_compile(uint32_t e, uint32_t h, uint32_t *w0, uint32_t *w1
           ((e & E_PEND) ? W1_PEND : 0u) | ((h & E_ASSERT) ? W1_ASSERT : 0u);
 }
 
-/* the whole table, compiled: tab[2 * i] = W0, tab[2 * i + 1] = W1 */
+/* the whole table, compiled: tab[2 * i] = W0, tab[2 * i + 1] = W1, then the header: one
+ * byte per op', lo | width << 5 of its field of C (DT_TABLE_WORDS words in all) */
 static inline void dt_build(uint32_t *tab) {
     for (uint32_t op = 0; op < DT_NOPS; ++op)
         for (uint32_t sub = 0; sub < DT_STRIDE; ++sub) {
@@ -289,6 +296,12 @@ static inline void dt_build(uint32_t *tab) {
             dt_entry(op, sub, &e, &h);
             dt_compile(e, h, &tab[2 * (op * DT_STRIDE + sub)], &tab[2 * (op * DT_STRIDE + sub) + 1]);
         }
+    for (uint32_t i = 0; i < DT_HDR_WORDS; ++i) tab[2 * DT_ENTRIES + i] = 0;
+    for (uint32_t op = 0; op < DT_NOPS; ++op) {
+        const uint32_t cls = (op < 10) ? ((DT_KCLS0 >> (3 * op)) & 7u) : ((DT_KCLS1 >> (3 * (op - 10))) & 7u);
+        const uint32_t hdr = ((DT_KLO >> (4 * cls)) & 15u) | (((DT_KW >> (4 * cls)) & 15u) << 5);
+        tab[2 * DT_ENTRIES + op / 4] |= hdr << (8 * (op % 4));
+    }
 }
 
 /* ---- the datapath (host + device) ----------------------------------------------------- */
@@ -338,27 +351,31 @@ DSM_HD uint32_t dt_ubfe(uint32_t x, uint32_t lo, uint32_t w) {
 #endif
 }
 
-DSM_HD uint32_t dt_index(const DtIn &in, uint32_t *evDb_out, uint32_t *own_out) {
+/* op': the message type / issue op, EVICT_SHARED at its home as DT_EVSH, an instruction
+ * whose home is not simulated as DT_ASSERT (:602) */
+DSM_HD uint32_t dt_opx(const DtIn &in) {
+    const uint32_t H = in.a >> 4;
+    uint32_t opx = in.op;
+    opx = (opx == DT_EVS && H == in.node) ? DT_EVSH : opx;
+    opx = (opx == DT_RD && !((in.np_mask >> H) & 1u)) ? DT_ASSERT : opx;
+    return opx;
+}
+
+/* table index of op' (header byte hdr = dt_hdr) for this lane's conditions */
+DSM_HD uint32_t dt_index(const DtIn &in, uint32_t opx, uint32_t hdr, uint32_t *evDb_out) {
     const uint32_t H = in.a >> 4;
     const uint32_t home = (H == in.node), hit = (in.La == in.a);
-    const uint32_t sbit = 1u << in.s;
-    const uint32_t ob = in.Db & in.np_mask;
-    const uint32_t own = (uint32_t)__builtin_ctz(ob | 0x80000000u);           /* findOwner */
-    const uint32_t evDb = in.Db & ~sbit;
+    const uint32_t evDb = in.Db & ~(1u << in.s);
     const uint32_t rem = (uint32_t)__builtin_popcount(evDb & in.np_mask);    /* countSharers */
-    uint32_t opx = in.op;
-    opx = (opx == DT_EVS && home) ? DT_EVSH : opx;
-    opx = (opx == DT_RD && !((in.np_mask >> H) & 1u)) ? DT_ASSERT : opx;                    /* :602 */
-    const uint32_t x = (in.op == DT_EVS) ? (uint32_t)(in.s == H) : in.excl;
-    const uint32_t C = x | (hit << 1) | (in.Ls << 2) | (home << 4) | ((uint32_t)(in.node == in.r2) << 5) |
-                       ((uint32_t)(own != in.s) << 6) | (in.Ds << 7) | (((in.Db >> in.s) & 1u) << 9) |
-                       ((uint32_t)(rem == 0) << 10) | ((uint32_t)(rem == 1) << 11);
-    const uint32_t cls = (uint32_t)((((uint64_t)DT_KCLS1 << 30) | DT_KCLS0) >> (3 * opx)) & 7u;
-    const uint32_t lo = (DT_KLO >> (4 * cls)) & 15u, w = (DT_KW >> (4 * cls)) & 15u;
-    const uint32_t sub = dt_ubfe(C, lo, w);
+    const uint32_t C = in.excl | (hit << 1) | (in.Ls << 2) | (home << 4) | ((uint32_t)(in.node == in.r2) << 5) |
+                       (in.Ds << 6) | (dt_ubfe(in.Db, in.s, 1) << 8) | ((rem < 2u ? rem : 2u) << 9);
     *evDb_out = evDb;
-    *own_out = own;
-    return opx * DT_STRIDE + sub;
+    return opx * DT_STRIDE + dt_ubfe(C, hdr & 31u, hdr >> 5);
+}
+
+/* header byte of op' (host side; the kernel reads it from the table's header in LDS) */
+static inline uint32_t dt_hdr(const uint32_t *tab, uint32_t opx) {
+    return (tab[2 * DT_ENTRIES + opx / 4] >> (8 * (opx % 4))) & 0xFFu;
 }
 
 /* v_perm_b32: byte i of the result = byte sel_i of {hi (bytes 4-7), lo (bytes 0-3)}; 12 = 0 */
@@ -377,7 +394,7 @@ DSM_HD uint32_t dt_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
 #endif
 }
 
-DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb, uint32_t own) {
+DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb) {
     DtOut o;
     const uint32_t H = in.a >> 4, sbit = 1u << in.s;
     /* the four byte results in one byte permute */
@@ -403,6 +420,7 @@ DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb, u
     const uint32_t dc = (W1 >> 10) & 7u;
     const bool d0 = dc & 1u, d1 = dc & 2u, d2 = dc & 4u;
     const uint32_t ctzEv = (uint32_t)__builtin_ctz((evDb & in.np_mask) | 0x80000000u);
+    const uint32_t own = (uint32_t)__builtin_ctz((in.Db & in.np_mask) | 0x80000000u);  /* findOwner */
     const uint32_t didx = d1 ? (d0 ? ctzEv : (in.La >> 4)) : (d0 ? own : in.s);
     const uint32_t mset = d0 ? (in.v & in.np_mask & ~(1u << in.node)) : ((1u << H) | (1u << in.r2));
     const uint32_t dm = d2 ? mset : (1u << didx);

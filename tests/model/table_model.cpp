@@ -82,13 +82,18 @@ int run_one(Sys &y, const uint32_t *tab, const Src &src, dsm_res *res) {
             in.op = op; in.node = (uint32_t)me; in.np_mask = npm;
             in.La = s.cache_addr[idx]; in.Lv = s.cache_value[idx]; in.Ls = s.cache_state[idx];
             in.Db = s.dir_bv[blk]; in.Ds = s.dir_state[blk]; in.Mv = s.memory[blk]; in.pend = s.pending;
-            uint32_t evDb, own;
-            const uint32_t ti = dt_index(in, &evDb, &own);
-            const DtOut o = dt_apply(in, tab[2 * ti], tab[2 * ti + 1], evDb, own);
+            uint32_t evDb;
+            const uint32_t opx = dt_opx(in);
+            const uint32_t ti = dt_index(in, opx, dt_hdr(tab, opx), &evDb);
+            const DtOut o = dt_apply(in, tab[2 * ti], tab[2 * ti + 1], evDb);
             s.cache_addr[idx] = (uint8_t)o.nLa; s.cache_value[idx] = (uint8_t)o.nLv;
             s.cache_state[idx] = (uint8_t)o.nLs;
             if (o.nLs != DT_CI && o.nLa == 0xFFu) {     /* the invariant dt_compile relies on */
                 fprintf(stderr, "valid line with address 0xFF\n");
+                abort();
+            }
+            if (o.nDs == DT_DEM && __builtin_popcount(o.nDb & npm) != 1) {   /* and dt_index */
+                fprintf(stderr, "directory entry in state EM without exactly one bit\n");
                 abort();
             }
             s.dir_bv[blk] = (uint8_t)o.nDb; s.dir_state[blk] = (uint8_t)o.nDs;
@@ -155,7 +160,7 @@ int main(int argc, char **argv) {
                         "       table_model packed np stride n traces counts ring out\n");
         return 1;
     }
-    static uint32_t tab[2 * DT_ENTRIES];
+    static uint32_t tab[DT_TABLE_WORDS];
     dt_build(tab);
     const int np = atoi(argv[2]);
     Sys *y = (Sys *)calloc(1, sizeof(Sys));
