@@ -424,11 +424,13 @@ DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb) {
     const uint32_t didx = d1 ? (d0 ? ctzEv : (in.La >> 4)) : (d0 ? own : in.s);
     const uint32_t mset = d0 ? (in.v & in.np_mask & ~(1u << in.node)) : ((1u << H) | (1u << in.r2));
     const uint32_t dm = d2 ? mset : (1u << didx);
-    o.o0 = (W1 & W1_O0) ? (lo16 | (W1 & (W1_X | W1_T(15))) | (r2f << 20) | (dm << 24)) : 0u;
+    /* a word is sent iff its destination mask is non-zero; the body of an unsent word is
+     * never read, so both words are computed unconditionally (no branch) */
+    o.o0 = lo16 | (W1 & (W1_X | W1_T(15))) | (r2f << 20) | ((dm & (0u - ((W1 >> 7) & 1u))) << 24);
     /* second outgoing word: the request to the home (type RREQ 0 / WREQ 1 / UPGRADE 6) */
     const uint32_t c1 = (W1 >> 27) & 3u;
-    o.o1 = c1 ? ((((0x6100u >> (4 * c1)) & 15u) << 16) | (in.a << 8) | ((W1 & W1_O1V) ? in.v : 0u) |
-                 (1u << (24 + H))) : 0u;
+    o.o1 = (((0x6100u >> (4 * c1)) & 15u) << 16) | (in.a << 8) | ((W1 & W1_O1V) ? in.v : 0u) |
+           (c1 ? (1u << (24 + H)) : 0u);
     /* node control word (pending byte, wait bit 8, assert bit 11): ctl' = ctl & ~cclr | cset */
     const uint32_t pm = (W1 & W1_PEND) ? 0xFFu : 0u;
     o.cset = ((W1 >> 12) & (DT_CTL_WAIT | DT_CTL_ASSERT)) | (in.v & pm);   /* WSET, ASSERT */
