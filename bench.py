@@ -283,7 +283,7 @@ def main():
         ach = alg_bytes / (kavg * 1e-3) / 1e9
         roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
-                    kernel="sim_kernel<8, 12, 4, false, false, 5> (lock-step transition kernel; 4-wave groups, ring 12, packed traces)",
+                    kernel="sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel; 4-wave groups, ring 12, packed traces)",
                     algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),
                     per_unit="2 B per consumed packed instruction + 32 B result + 4*np B counts per system")
         tr = traffic_from_profiles(args.config) or {}
