@@ -37,7 +37,12 @@ for r in range(reps):
         eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
         ms = eng.last_kernel_ms()
         torch.cuda.synchronize()
-        c = pydsm.counters_to_dict(cnt.cpu().numpy().view(np.uint64))
+        raw = cnt.cpu().numpy().view(np.uint64)
+        c = pydsm.counters_to_dict(raw)
+        if os.environ.get("DSM_PRINT_RAW"):     # probe builds: section clocks in slots 27-31
+            wr = int(raw[26])
+            print(f"{v}: wave_rounds {wr} section clocks/wave-round "
+                  f"{[round(int(x) / max(wr, 1), 1) for x in raw[27:32]]}", flush=True)
         key = (c["msgs"], c["sum_final_hash"], c["sum_dump_hash"])
         ref = ref or key
         assert key == ref, (v, key, ref)
