@@ -57,7 +57,7 @@ struct SimArgs {
     unsigned int *claim;            /* 8 shard counters, 32 words apart                     */
     uint32_t *ovf_list;             /* fast kernel: systems handed to the 256-deep re-run   */
     unsigned int *ovf_count;
-    const uint2 *table;             /* micro-op table (dsm_table.h), DT_ENTRIES entries     */
+    const uint2 *table;             /* micro-op table (dsm_table.h), DT_TABLE_WORDS words   */
     uint64_t sched_seed;            /* M_SX: seeded schedule exploration (dsm_set_schedule)  */
     uint32_t sched_thresh;
     uint32_t issue_cap;             /* M_TR: events per system                               */
@@ -87,10 +87,10 @@ enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17,
        K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_N = 32 };
 
 constexpr uint64_t NO_SYS = ~0ull;
+constexpr uint32_t DSM_LINE_INIT = 0xFFu | (3u << 16);   /* address 0xFF, value 0, INVALID */
 constexpr int FB_RING = 256;        /* MSG_BUFFER_SIZE, assignment.c:12 */
 
 /* ---- small bit-field helpers ------------------------------------------------------- */
-DEVI uint32_t get8(uint32_t w, uint32_t i) { return __builtin_amdgcn_ubfe(w, i * 8, 8); }
 DEVI uint32_t get2(uint32_t w, uint32_t i) { return __builtin_amdgcn_ubfe(w, i * 2, 2); }
 DEVI uint32_t set2(uint32_t w, uint32_t i, uint32_t v) {
     const uint32_t sh = i * 2;
@@ -108,9 +108,6 @@ DEVI uint64_t fmix64(uint64_t z) {
 }
 struct Node {
     uint32_t dst;     /* directory states, 2 bits per block                                 */
-    uint32_t caddr;   /* cache addresses, one byte per line                                 */
-    uint32_t cval;    /* cache values                                                       */
-    uint32_t cst;     /* cache states, 2 bits per line                                      */
     uint32_t ctl;     /* pending | C_* flags                                                */
     uint32_t ip;      /* instructions issued                                                */
     uint32_t nins;    /* instructions in this node's trace                                  */
@@ -119,18 +116,20 @@ struct Node {
 };
 
 /* canonical 64-byte record (dsm_node_state) word i; mem / bv words come from LDS */
-DEVI uint32_t rec_word(const Node &nd, const uint32_t (&mb)[8], uint32_t flags, int i) {
+DEVI uint32_t rec_word(const Node &nd, const uint32_t (&mb)[8], const uint32_t (&ln)[4], uint32_t flags, int i) {
     switch (i) {
     case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 7: return mb[i];
     case 8: case 9: case 10: case 11: {
         const uint32_t e = nd.dst >> (8 * (i - 8));
         return (e & 3u) | (((e >> 2) & 3u) << 8) | (((e >> 4) & 3u) << 16) | (((e >> 6) & 3u) << 24);
     }
-    case 12: return nd.caddr;
-    case 13: return nd.cval;
+    case 12: return __builtin_amdgcn_perm(__builtin_amdgcn_perm(ln[3], ln[2], 0x0C0C0400u),
+                                          __builtin_amdgcn_perm(ln[1], ln[0], 0x0C0C0400u), 0x05040100u);
+    case 13: return __builtin_amdgcn_perm(__builtin_amdgcn_perm(ln[3], ln[2], 0x0C0C0501u),
+                                          __builtin_amdgcn_perm(ln[1], ln[0], 0x0C0C0501u), 0x05040100u);
     case 14:
-        return (nd.cst & 3u) | (((nd.cst >> 2) & 3u) << 8) | (((nd.cst >> 4) & 3u) << 16) |
-               (((nd.cst >> 6) & 3u) << 24);
+        return __builtin_amdgcn_perm(__builtin_amdgcn_perm(ln[3], ln[2], 0x0C0C0602u),
+                                     __builtin_amdgcn_perm(ln[1], ln[0], 0x0C0C0602u), 0x05040100u);
     default: return (nd.ctl & 0xFFu) | (flags << 8) | (nd.ip << 16);
     }
 }
@@ -149,15 +148,16 @@ DEVI void load_mb(const uint32_t (&smb)[WAVES][8][64], uint32_t wv, uint32_t lan
 /* store this lane's 64-byte node record (dsm_node_state) */
 template <int WAVES>
 DEVI void store_rec(uint4 *dst, const Node &nd, const uint32_t (&smb)[WAVES][8][64],
-                    uint32_t wv, uint32_t lane, uint32_t flags) {
+                    const uint32_t (&sln)[WAVES][4][64], uint32_t wv, uint32_t lane, uint32_t flags) {
+    const uint32_t ln[4] = {sln[wv][0][lane], sln[wv][1][lane], sln[wv][2][lane], sln[wv][3][lane]};
     uint32_t mb[8];
     load_mb<WAVES>(smb, wv, lane, mb);
     dst[0] = make_uint4(mb[0], mb[1], mb[2], mb[3]);
     dst[1] = make_uint4(mb[4], mb[5], mb[6], mb[7]);
-    dst[2] = make_uint4(rec_word(nd, mb, flags, 8), rec_word(nd, mb, flags, 9),
-                        rec_word(nd, mb, flags, 10), rec_word(nd, mb, flags, 11));
-    dst[3] = make_uint4(rec_word(nd, mb, flags, 12), rec_word(nd, mb, flags, 13),
-                        rec_word(nd, mb, flags, 14), rec_word(nd, mb, flags, 15));
+    dst[2] = make_uint4(rec_word(nd, mb, ln, flags, 8), rec_word(nd, mb, ln, flags, 9),
+                        rec_word(nd, mb, ln, flags, 10), rec_word(nd, mb, ln, flags, 11));
+    dst[3] = make_uint4(rec_word(nd, mb, ln, flags, 12), rec_word(nd, mb, ln, flags, 13),
+                        rec_word(nd, mb, ln, flags, 14), rec_word(nd, mb, ln, flags, 15));
 }
 
 template <int NP>
@@ -209,6 +209,7 @@ sim_kernel(const SimArgs *Ap) {
     constexpr bool TC = (MODE & M_TC) != 0, TR = (MODE & M_TR) != 0, SX = (MODE & M_SX) != 0;
 
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
+    __shared__ uint32_t s_line[WAVES][4][64];        /* cache lines: addr | value << 8 | state << 16 */
     __shared__ uint32_t s_ring[WAVES][RING][64];                       /* inbox rings   */
     __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][128]; /* 2 words/lane  */
     __shared__ uint32_t s_rm[WAVES][64];                               /* receive masks */
@@ -242,7 +243,7 @@ sim_kernel(const SimArgs *Ap) {
     uint32_t nev = 0;                          /* TR: issue events of the system so far */
     const uint64_t smul = SX ? Ap->sched_seed * 0x9E3779B97F4A7C15ULL : 0;
     const uint32_t sthr = SX ? Ap->sched_thresh : 0;
-    nd.dst = nd.caddr = nd.cval = nd.cst = nd.ctl = nd.ip = nd.nins = nd.rh = nd.nmsg = 0;
+    nd.dst = nd.ctl = nd.ip = nd.nins = nd.rh = nd.nmsg = 0;
 
     /* initializeProcessor :778-790 and main :142-146 for a new system in this lane's group */
     auto start = [&](uint64_t s) {
@@ -250,7 +251,9 @@ sim_kernel(const SimArgs *Ap) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             s_mb[wv][i][lane] = ((20u * node + 2 * i) & 0xFFu) | (((20u * node + 2 * i + 1) & 0xFFu) << 16);
-        nd.dst = 0xAAAAAAAAu; nd.caddr = 0xFFFFFFFFu; nd.cval = 0; nd.cst = 0xFFu;
+        nd.dst = 0xAAAAAAAAu;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s_line[wv][i][lane] = DSM_LINE_INIT;
         nd.ctl = 0; nd.ip = 0; nd.rh = 0; nd.nmsg = 0;
         rounds = 0;
         nev = 0;
@@ -340,23 +343,19 @@ sim_kernel(const SimArgs *Ap) {
         uint16_t *const mbp = reinterpret_cast<uint16_t *>(&s_mb[wv][blk >> 1][lane]) + (blk & 1u);
         const uint32_t mbw = *mbp;
         in.op = op; in.node = node; in.np_mask = NPM;
-        in.La = get8(nd.caddr, idx); in.Lv = get8(nd.cval, idx); in.Ls = get2(nd.cst, idx);
+        const uint32_t lw = s_line[wv][idx][lane];
+        in.La = lw & 0xFFu; in.Lv = (lw >> 8) & 0xFFu; in.Ls = lw >> 16;
         in.Db = mbw >> 8; in.Ds = get2(nd.dst, blk); in.Mv = mbw & 0xFFu; in.pend = nd.ctl & 0xFFu;
         uint32_t evDb;
         const uint32_t opx = dt_opx(in);
-        const uint32_t hdr = reinterpret_cast<const uint8_t *>(&s_tab[DT_ENTRIES])[opx];
-        const uint32_t ti = dt_index(in, opx, hdr, &evDb);
+        const uint32_t hdr = reinterpret_cast<const uint32_t *>(&s_tab[DT_ENTRIES])[opx];
+        const uint32_t ti = dt_index(in, hdr, &evDb);
         const uint2 E = s_tab[ti];
         const DtOut o = dt_apply(in, E.x, E.y, evDb);
         const uint32_t o0 = o.o0, o1 = o.o1;
 
         /* ---- (3) write back (idle lanes rewrite unchanged values) ------------------- */
-        {   /* line.address / line.value bytes 0 / 1 of o.P into byte idx of caddr / cval */
-            const uint32_t sa = 0x03020100u + ((4u - idx) << (8 * idx));
-            nd.caddr = __builtin_amdgcn_perm(o.P, nd.caddr, sa);
-            nd.cval = __builtin_amdgcn_perm(o.P, nd.cval, sa + (1u << (8 * idx)));
-        }
-        nd.cst = set2(nd.cst, idx, o.nLs);
+        s_line[wv][idx][lane] = __builtin_amdgcn_perm(o.S, o.P, 0x0C040100u);   /* nLa nLv nLs */
         nd.dst = set2(nd.dst, blk, o.nDs);
         *mbp = (uint16_t)(o.nMv | (o.nDb << 8));
         nd.ctl = (nd.ctl & ~o.cclr) | o.cset;      /* wait, pendingWriteValue (:633), assert */
@@ -369,7 +368,7 @@ sim_kernel(const SimArgs *Ap) {
         }
         if (doDump) {                                                    /* :688-697 */
             nd.ctl |= C_DUMPED;               /* printProcessorState(threadId, node), :695 */
-            store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8, nd, s_mb, wv, lane, 2u);
+            store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8, nd, s_mb, s_line, wv, lane, 2u);
         }
 
         /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
@@ -449,7 +448,7 @@ sim_kernel(const SimArgs *Ap) {
                 else st = DSM_ROUND_LIMIT;
                 const bool handoff = !FB && (st == DSM_RING_OVERFLOW);
                 const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
-                if (!handoff) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, wv, lane, fl);
+                if (!handoff) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
                 const uint32_t ins = gsum32<NP>(nd.ip), msgs = gsum32<NP>(nd.nmsg);
                 uint32_t nlo = 0xFFFFFFFFu, nhi = 0xFFFFFFFFu;
                 if (node == 0) {
@@ -684,7 +683,7 @@ sim_fn pick_fallback(int np, bool gen, int mode) {
     return gen ? fb_np_gen<8, true>(mode) : fb_np_gen<8, false>(mode);
 }
 int lds_bytes(int ring, int waves) {
-    return waves * (8 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 4 + K_N * 8) + DT_TABLE_WORDS * 4;
+    return waves * (8 * 64 * 4 + 4 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 4 + K_N * 8) + DT_TABLE_WORDS * 4;
 }
 
 }  // namespace
@@ -742,8 +741,7 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     }
     {
         static uint32_t tab[DT_TABLE_WORDS];
-        dt_build(tab);
-        if (hipMemcpy(c->d_table, tab, sizeof tab, hipMemcpyHostToDevice) != hipSuccess) {
+        if (dt_build(tab) > DT_ENTRIES || hipMemcpy(c->d_table, tab, sizeof tab, hipMemcpyHostToDevice) != hipSuccess) {
             dsm_close(c);
             return DSM_E_DEVICE;
         }

@@ -22,8 +22,9 @@
  *   op' = the message type / issue op, with EVICT_SHARED at its home as its own op (17)
  *         and an unsimulatable instruction (home >= np) as ASSERT (18);
  *   each op' reads one contiguous bit-field of C (its class: lo, width; a byte per op' in
- *   the table's header, dt_hdr), so index = op' * 32 + bfe(C, lo, width) -- no per-op
- *   branch anywhere.
+ *   the table's header, dt_hdr, with the op's first row), so index = base(op') +
+ *   bfe(C, lo, width) -- no per-op branch anywhere.  The rows are packed: an op reading a
+ *   w-bit field owns 2^w rows (268 rows in all).
  *
  * An entry (64 bits) says what to do with the cache line, the directory entry, the memory
  * byte, the two outgoing message words (templates whose operands are picked from a few
@@ -48,8 +49,9 @@ enum : uint32_t {
     DT_RREQ = 0, DT_WREQ = 1, DT_RRD = 2, DT_RWR = 3, DT_RID = 4, DT_INV = 5, DT_UPG = 6,
     DT_WBINV = 7, DT_WBINT = 8, DT_FLUSH = 9, DT_FLINV = 10, DT_EVS = 11, DT_EVM = 12,
     DT_RD = 13, DT_WR = 14, DT_DUMP = 15, DT_IDLE = 16, DT_EVSH = 17, DT_ASSERT = 18,
-    DT_NOPS = 20, DT_STRIDE = 32, DT_ENTRIES = DT_NOPS * DT_STRIDE,
-    DT_HDR_WORDS = 8, DT_TABLE_WORDS = 2 * DT_ENTRIES + DT_HDR_WORDS
+    DT_NOPS = 20, DT_STRIDE = 32,
+    DT_ENTRIES = 320,                       /* row capacity (dt_build packs 268 rows)      */
+    DT_HDR_WORDS = 32, DT_TABLE_WORDS = 2 * DT_ENTRIES + DT_HDR_WORDS
 };
 enum : uint32_t { DT_CM = 0, DT_CE = 1, DT_CS = 2, DT_CI = 3 };   /* cacheLineState :17 */
 enum : uint32_t { DT_DEM = 0, DT_DS = 1, DT_DU = 2 };             /* directoryEntryState :18 */
@@ -287,21 +289,23 @@ static inline void dt_compile(uint32_t e, uint32_t h, uint32_t *w0, uint32_t *w1
           ((e & E_PEND) ? W1_PEND : 0u) | ((h & E_ASSERT) ? W1_ASSERT : 0u);
 }
 
-/* the whole table, compiled: tab[2 * i] = W0, tab[2 * i + 1] = W1, then the header: one
- * byte per op', lo | width << 5 of its field of C (DT_TABLE_WORDS words in all) */
-static inline void dt_build(uint32_t *tab) {
-    for (uint32_t op = 0; op < DT_NOPS; ++op)
-        for (uint32_t sub = 0; sub < DT_STRIDE; ++sub) {
-            uint32_t e, h;
-            dt_entry(op, sub, &e, &h);
-            dt_compile(e, h, &tab[2 * (op * DT_STRIDE + sub)], &tab[2 * (op * DT_STRIDE + sub) + 1]);
-        }
-    for (uint32_t i = 0; i < DT_HDR_WORDS; ++i) tab[2 * DT_ENTRIES + i] = 0;
+/* the whole table, compiled: rows tab[2 * i] = W0, tab[2 * i + 1] = W1, packed op after op
+ * (an op with a w-bit field owns 2^w rows), then the header: one word per op',
+ * lo | width << 5 | first row << 16 (DT_TABLE_WORDS words in all) */
+static inline uint32_t dt_build(uint32_t *tab) {
+    for (uint32_t i = 0; i < DT_TABLE_WORDS; ++i) tab[i] = 0;
+    uint32_t row = 0;
     for (uint32_t op = 0; op < DT_NOPS; ++op) {
         const uint32_t cls = (op < 10) ? ((DT_KCLS0 >> (3 * op)) & 7u) : ((DT_KCLS1 >> (3 * (op - 10))) & 7u);
-        const uint32_t hdr = ((DT_KLO >> (4 * cls)) & 15u) | (((DT_KW >> (4 * cls)) & 15u) << 5);
-        tab[2 * DT_ENTRIES + op / 4] |= hdr << (8 * (op % 4));
+        const uint32_t lo = (DT_KLO >> (4 * cls)) & 15u, w = (DT_KW >> (4 * cls)) & 15u;
+        tab[2 * DT_ENTRIES + op] = lo | (w << 5) | (row << 16);
+        for (uint32_t sub = 0; sub < (1u << w); ++sub, ++row) {
+            uint32_t e, h;
+            dt_entry(op, sub, &e, &h);
+            if (row < DT_ENTRIES) dt_compile(e, h, &tab[2 * row], &tab[2 * row + 1]);
+        }
     }
+    return row;                                  /* rows used; must not exceed DT_ENTRIES */
 }
 
 /* ---- the datapath (host + device) ----------------------------------------------------- */
@@ -316,6 +320,7 @@ struct DtIn {
 struct DtOut {
     uint32_t nLa, nLv, nLs, nDb, nDs, nMv;
     uint32_t P;                        /* bytes nLa, nLv, nMv, payload                    */
+    uint32_t S;                        /* bytes nLs, -, -, nDs                            */
     uint32_t o0, o1;                   /* outgoing words: body | destination mask << 24   */
     bool wset, wclr;                   /* waitingForReply := 1 / := 0                     */
     bool pendw;                        /* pendingWriteValue := v                          */
@@ -361,8 +366,8 @@ DSM_HD uint32_t dt_opx(const DtIn &in) {
     return opx;
 }
 
-/* table index of op' (header byte hdr = dt_hdr) for this lane's conditions */
-DSM_HD uint32_t dt_index(const DtIn &in, uint32_t opx, uint32_t hdr, uint32_t *evDb_out) {
+/* table row of op' (header word hdr = dt_hdr) for this lane's conditions */
+DSM_HD uint32_t dt_index(const DtIn &in, uint32_t hdr, uint32_t *evDb_out) {
     const uint32_t H = in.a >> 4;
     const uint32_t home = (H == in.node), hit = (in.La == in.a);
     const uint32_t evDb = in.Db & ~(1u << in.s);
@@ -370,13 +375,11 @@ DSM_HD uint32_t dt_index(const DtIn &in, uint32_t opx, uint32_t hdr, uint32_t *e
     const uint32_t C = in.excl | (hit << 1) | (in.Ls << 2) | (home << 4) | ((uint32_t)(in.node == in.r2) << 5) |
                        (in.Ds << 6) | (dt_ubfe(in.Db, in.s, 1) << 8) | ((rem < 2u ? rem : 2u) << 9);
     *evDb_out = evDb;
-    return opx * DT_STRIDE + dt_ubfe(C, hdr & 31u, hdr >> 5);
+    return (hdr >> 16) + dt_ubfe(C, hdr & 31u, (hdr >> 5) & 7u);
 }
 
-/* header byte of op' (host side; the kernel reads it from the table's header in LDS) */
-static inline uint32_t dt_hdr(const uint32_t *tab, uint32_t opx) {
-    return (tab[2 * DT_ENTRIES + opx / 4] >> (8 * (opx % 4))) & 0xFFu;
-}
+/* header word of op' (host side; the kernel reads it from the table's header in LDS) */
+static inline uint32_t dt_hdr(const uint32_t *tab, uint32_t opx) { return tab[2 * DT_ENTRIES + opx]; }
 
 /* v_perm_b32: byte i of the result = byte sel_i of {hi (bytes 4-7), lo (bytes 0-3)}; 12 = 0 */
 DSM_HD uint32_t dt_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
@@ -407,6 +410,7 @@ DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb) {
     o.nMv = (P >> 16) & 0xFFu;
     /* line and directory states: a permute of {Ls, Ds} and the constants 0..3 */
     const uint32_t S = dt_perm(0x03020100u, in.Ls | (in.Ds << 8), W1 & (W1_LSEL(7) | W1_DSEL(7)));
+    o.S = S;
     o.nLs = S & 0xFFu;
     o.nDs = S >> 24;
     const uint32_t db = (W1 >> 5) & 3u;

@@ -84,7 +84,7 @@ int run_one(Sys &y, const uint32_t *tab, const Src &src, dsm_res *res) {
             in.Db = s.dir_bv[blk]; in.Ds = s.dir_state[blk]; in.Mv = s.memory[blk]; in.pend = s.pending;
             uint32_t evDb;
             const uint32_t opx = dt_opx(in);
-            const uint32_t ti = dt_index(in, opx, dt_hdr(tab, opx), &evDb);
+            const uint32_t ti = dt_index(in, dt_hdr(tab, opx), &evDb);
             const DtOut o = dt_apply(in, tab[2 * ti], tab[2 * ti + 1], evDb);
             s.cache_addr[idx] = (uint8_t)o.nLa; s.cache_value[idx] = (uint8_t)o.nLv;
             s.cache_state[idx] = (uint8_t)o.nLs;
@@ -161,7 +161,10 @@ int main(int argc, char **argv) {
         return 1;
     }
     static uint32_t tab[DT_TABLE_WORDS];
-    dt_build(tab);
+    if (dt_build(tab) > DT_ENTRIES) {
+        fprintf(stderr, "micro-op table rows exceed DT_ENTRIES\n");
+        return 1;
+    }
     const int np = atoi(argv[2]);
     Sys *y = (Sys *)calloc(1, sizeof(Sys));
     y->np = np;
