@@ -279,6 +279,8 @@ sim_kernel(const SimArgs *Ap) {
     if (G < n) {
         live = true;
         start(G);
+    } else {
+        nd.ctl = C_WAIT | C_DUMPED;              /* a dead lane never acts (step (1)) */
     }
 
     uint32_t wrounds = 0;    /* loop iterations of this wave (uniform) */
@@ -288,11 +290,16 @@ sim_kernel(const SimArgs *Ap) {
         ++wrounds;
 
         /* ---- (1) this round's action, from state at the start of the round ---------- */
+        /* A dead lane holds an empty inbox and C_WAIT | C_DUMPED, so it never acts.  One
+         * compare gives "inbox empty and not waiting": the count sits at bits 8+ of rh, the
+         * flags at bits 8-11 of ctl.  C_DUMPED there is harmless (a dumped node has issued
+         * every instruction and dumps once), and so are C_OVF / C_ASSERT (their system ends
+         * in the round that sets them). */
         const uint32_t cnt0 = nd.rh >> 8, head0 = nd.rh & 0xFFu;
-        bool hasMsg = live && cnt0 != 0;                                  /* :158-169 */
-        const bool canIssue = live && !hasMsg && !(nd.ctl & C_WAIT);      /* :578-581 */
+        bool hasMsg = cnt0 != 0;                                          /* :158-169 */
+        const bool canIssue = (nd.rh | nd.ctl) < 256u;                    /* :578-581 */
         bool doIssue = canIssue && nd.ip < nd.nins;                       /* :590-592 */
-        bool doDump = canIssue && !doIssue && !(nd.ctl & C_DUMPED);       /* :688-697 */
+        bool doDump = canIssue && nd.ip >= nd.nins;                       /* :688-697 */
         bool stall = false;
         if (SX) {           /* a node with an action may stall this round (dsm_sched_act) */
             const bool avail = hasMsg || doIssue || doDump;
@@ -422,8 +429,12 @@ sim_kernel(const SimArgs *Ap) {
          * with no active lane (a zero field in actb | ~liveb), or a lane with an assert, an
          * overflow or the round limit; the per-lane finish runs only then. */
         ++rounds;
-        const uint64_t actb = __ballot(op != OP_IDLE || stall);    /* stalled = available */
-        const uint64_t flagb = __ballot((nd.ctl & (C_ASSERT | C_OVF)) || rounds >= DSM_MAX_ROUNDS);
+        /* both tests on VGPR integers (one compare each; DSM_MAX_ROUNDS is a power of two) */
+        uint32_t opv = op;
+        asm volatile("" : "+v"(opv));
+        const uint64_t actb = __ballot(opv != OP_IDLE || stall);   /* stalled = available */
+        static_assert((DSM_MAX_ROUNDS & (DSM_MAX_ROUNDS - 1)) == 0, "DSM_MAX_ROUNDS");
+        const uint64_t flagb = __ballot(((nd.ctl & (C_ASSERT | C_OVF)) | (rounds / DSM_MAX_ROUNDS)) != 0u);
         constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
         constexpr uint64_t GHI = GLO << (NP - 1);
         const uint64_t t = actb | ~liveb;
@@ -495,8 +506,13 @@ sim_kernel(const SimArgs *Ap) {
                 nlo = __shfl(nlo, (int)gbase, 64);
                 nhi = __shfl(nhi, (int)gbase, 64);
                 const uint64_t nl = ((uint64_t)nhi << 32) | nlo;
-                if (nl != NO_SYS) start(nl);
-                else live = false;
+                if (nl != NO_SYS) {
+                    start(nl);
+                } else {
+                    live = false;
+                    nd.rh = 0;
+                    nd.ctl = C_WAIT | C_DUMPED;      /* never acts again (round step (1)) */
+                }
             }
         }
         liveb = __ballot(live);
