@@ -63,6 +63,14 @@ struct SimArgs {
     uint32_t issue_cap;             /* M_TR: events per system                               */
     uint32_t *issue;                /* M_TR: [sys][issue_cap] node << 16 | packed instruction */
     uint32_t *issue_n;              /* M_TR: [sys] events                                    */
+    /* two-pass schedule (run_engine): a budget pass suspends every system still running
+     * after 1 << rsh rounds, a resume pass continues them from their saved state */
+    uint32_t rsh;                   /* round-limit test: rounds >> rsh != 0                  */
+    uint32_t budget;                /* budget pass: suspend at 1 << rsh rounds               */
+    uint32_t resume;                /* resume pass: start() restores a suspended system      */
+    uint32_t *susp;                 /* [sys][word][node] suspended state (susp_words)        */
+    uint32_t *susp_list;            /* budget pass: suspended system ids                     */
+    unsigned int *susp_count;
 };
 
 
@@ -84,7 +92,12 @@ constexpr uint32_t C_WAIT = DT_CTL_WAIT, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C
 
 /* counter slots (dsm_counters order) */
 enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
-       K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_N = 32 };
+       K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_RESUMED = 27, K_N = 32 };
+constexpr uint32_t RSH_MAX = 22;    /* 1 << 22 == DSM_MAX_ROUNDS */
+static_assert((1u << RSH_MAX) == DSM_MAX_ROUNDS, "DSM_MAX_ROUNDS");
+/* suspended node state: memory/bitVector (8), lines (4), ring (RING), dst, ctl, ip, nins, rh,
+ * nmsg, rounds (7), trace chunks cur, nxt (8) */
+constexpr int susp_words(int ring) { return 27 + ring; }
 
 constexpr uint64_t NO_SYS = ~0ull;
 constexpr uint32_t DSM_LINE_INIT = 0xFFu | (3u << 16);   /* address 0xFF, value 0, INVALID */
@@ -207,6 +220,8 @@ sim_kernel(const SimArgs *Ap) {
     constexpr uint32_t NPM = (1u << NP) - 1u;
     constexpr bool FB = (RING == FB_RING);   /* the 256-deep re-run kernel                */
     constexpr bool TC = (MODE & M_TC) != 0, TR = (MODE & M_TR) != 0, SX = (MODE & M_SX) != 0;
+    constexpr bool BUD = MODE == 0 && !FB && !GEN;   /* the two-pass schedule's suspend/resume */
+    constexpr int SW = susp_words(RING);
 
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
     __shared__ uint32_t s_line[WAVES][4][64];        /* cache lines: addr | value << 8 | state << 16 */
@@ -232,6 +247,8 @@ sim_kernel(const SimArgs *Ap) {
     const uint64_t gfirst = GEN ? Ap->first_sys : 0;
     const int gdist = GEN ? Ap->dist : 0;
     const uint32_t stride = GEN ? 0u : Ap->stride;   /* >= 8, multiple of 8 (dsm_open) */
+    const uint32_t rsh = BUD ? Ap->rsh : RSH_MAX;
+    const bool budget = BUD && Ap->budget != 0, resume = BUD && Ap->resume != 0;
 
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
@@ -248,6 +265,23 @@ sim_kernel(const SimArgs *Ap) {
     /* initializeProcessor :778-790 and main :142-146 for a new system in this lane's group */
     auto start = [&](uint64_t s) {
         sys = list ? (uint64_t)list[s] : s;
+        if (resume) {                 /* continue a system the budget pass suspended */
+            const uint32_t *sp = Ap->susp + sys * (uint64_t)(SW * NP) + node;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s_mb[wv][i][lane] = sp[i * NP];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s_line[wv][i][lane] = sp[(8 + i) * NP];
+#pragma unroll
+            for (int i = 0; i < RING; ++i) s_ring[wv][i][lane] = sp[(12 + i) * NP];
+            const uint32_t *q = sp + (12 + RING) * NP;
+            nd.dst = q[0]; nd.ctl = q[NP]; nd.ip = q[2 * NP]; nd.nins = q[3 * NP];
+            nd.rh = q[4 * NP]; nd.nmsg = q[5 * NP]; rounds = q[6 * NP];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { cur[k] = q[(7 + k) * NP]; nxt[k] = q[(11 + k) * NP]; }
+            tb = Ap->traces + (sys * NP + node) * (uint64_t)stride;
+            rmsg = s_ring[wv][nd.rh & 0xFFu][lane];          /* the head, as the loop keeps it */
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             s_mb[wv][i][lane] = ((20u * node + 2 * i) & 0xFFu) | (((20u * node + 2 * i + 1) & 0xFFu) << 16);
@@ -433,8 +467,8 @@ sim_kernel(const SimArgs *Ap) {
         uint32_t opv = op;
         asm volatile("" : "+v"(opv));
         const uint64_t actb = __ballot(opv != OP_IDLE || stall);   /* stalled = available */
-        static_assert((DSM_MAX_ROUNDS & (DSM_MAX_ROUNDS - 1)) == 0, "DSM_MAX_ROUNDS");
-        const uint64_t flagb = __ballot(((nd.ctl & (C_ASSERT | C_OVF)) | (rounds / DSM_MAX_ROUNDS)) != 0u);
+        /* rounds >> rsh: DSM_MAX_ROUNDS, or the budget pass's 1 << rsh */
+        const uint64_t flagb = __ballot(((nd.ctl & (C_ASSERT | C_OVF)) | (rounds >> rsh)) != 0u);
         constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
         constexpr uint64_t GHI = GLO << (NP - 1);
         const uint64_t t = actb | ~liveb;
@@ -443,7 +477,9 @@ sim_kernel(const SimArgs *Ap) {
         const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
         const bool gbad = ((badb >> gbase) & NPM) != 0;
         if (gact == 0) --rounds;
-        const bool done = live && (gact == 0 || gbad || rounds >= DSM_MAX_ROUNDS);
+        /* budget pass: a system still running after 1 << rsh rounds is suspended */
+        const bool susp = budget && gact != 0 && !gbad && rounds >= (1u << rsh);
+        const bool done = live && (gact == 0 || gbad || rounds >= DSM_MAX_ROUNDS || susp);
 
         const uint64_t doneb = __ballot(done);
         if (doneb) {
@@ -459,11 +495,29 @@ sim_kernel(const SimArgs *Ap) {
                 else st = DSM_ROUND_LIMIT;
                 const bool handoff = !FB && (st == DSM_RING_OVERFLOW);
                 const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
-                if (!handoff) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
+                if (!handoff && !susp) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
+                if (susp) {               /* save the node for the resume pass (start()) */
+                    uint32_t *sp = Ap->susp + sys * (uint64_t)(SW * NP) + node;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) sp[i * NP] = s_mb[wv][i][lane];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sp[(8 + i) * NP] = s_line[wv][i][lane];
+#pragma unroll
+                    for (int i = 0; i < RING; ++i) sp[(12 + i) * NP] = s_ring[wv][i][lane];
+                    uint32_t *q = sp + (12 + RING) * NP;
+                    q[0] = nd.dst; q[NP] = nd.ctl; q[2 * NP] = nd.ip; q[3 * NP] = nd.nins;
+                    q[4 * NP] = nd.rh; q[5 * NP] = nd.nmsg; q[6 * NP] = rounds;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) { q[(7 + k) * NP] = cur[k]; q[(11 + k) * NP] = nxt[k]; }
+                }
                 const uint32_t ins = gsum32<NP>(nd.ip), msgs = gsum32<NP>(nd.nmsg);
                 uint32_t nlo = 0xFFFFFFFFu, nhi = 0xFFFFFFFFu;
                 if (node == 0) {
-                    if (handoff) {
+                    if (susp) {
+                        const uint32_t pos = atomicAdd(Ap->susp_count, 1u);
+                        Ap->susp_list[pos] = (uint32_t)sys;
+                        atomicAdd(&s_cnt[wv][K_RESUMED], 1ull);
+                    } else if (handoff) {
                         const uint32_t pos = atomicAdd(Ap->ovf_count, 1u);
                         Ap->ovf_list[pos] = (uint32_t)sys;
                         atomicAdd(&s_cnt[wv][K_OVFRERUN], 1ull);
@@ -709,10 +763,29 @@ int lds_bytes(int ring, int waves) {
 /* ====================================================================================== */
 
 
-#define CTRL_WORDS 1024
+#define CTRL_WORDS 2048
 #define CTRL_FAST 0
 #define CTRL_FB 256
 #define CTRL_OVF 512
+#define CTRL_RES 1024       /* claim shards of the resume pass */
+#define CTRL_SUSP 1536      /* systems the budget pass suspended */
+
+/* Two-pass schedule (bench mode: MODE 0, packed traces).  A system's length is unknown until
+ * it ends, and ~14% of C3 systems run ~12.5k rounds against a median of ~650: in one
+ * persistent launch the long systems claimed last set the kernel's end at low occupancy.  The
+ * budget pass therefore runs every system for at most 1 << log2 rounds and suspends the rest
+ * (their state to HBM); the resume pass continues those (almost all long, of similar
+ * remaining length) on a grid sized to an integral number of systems per slot.  Results are
+ * identical: a system's rounds run in the same order, only split across two launches.
+ * DSM_BUDGET_LOG2 (environment) overrides the budget; 0 turns the schedule off. */
+static uint32_t budget_log2() {
+    const char *e = getenv("DSM_BUDGET_LOG2");
+    if (e && *e) {
+        const long v = strtol(e, nullptr, 10);
+        return (v > 0 && v < (long)RSH_MAX) ? (uint32_t)v : 0u;
+    }
+    return 12;
+}
 
 
 #define ensure dsm_ensure
@@ -747,8 +820,8 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void **)&c->d_ctrl, CTRL_WORDS * sizeof(unsigned int)) != hipSuccess ||
-        hipMalloc((void **)&c->d_args, 2 * sizeof(SimArgs)) != hipSuccess ||
-        hipHostMalloc((void **)&c->h_args, 2 * sizeof(SimArgs), hipHostMallocDefault) != hipSuccess ||
+        hipMalloc((void **)&c->d_args, 3 * sizeof(SimArgs)) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_args, 3 * sizeof(SimArgs), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_args, hipEventDisableTiming) != hipSuccess ||
         hipMalloc((void **)&c->d_cnt, sizeof(dsm_counters)) != hipSuccess ||
         hipMalloc((void **)&c->d_table, DT_TABLE_WORDS * sizeof(uint32_t)) != hipSuccess) {
@@ -775,7 +848,8 @@ extern "C" void dsm_close(dsm_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *ptrs[] = {c->d_ctrl, c->d_args, c->d_partials, c->d_ovf_list, c->d_traces, c->d_counts,
+    void *ptrs[] = {c->d_ctrl, c->d_args, c->d_partials, c->d_ovf_list, c->d_susp, c->d_susp_list,
+                    c->d_traces, c->d_counts,
                     c->d_res, c->d_cnt, c->d_recs, c->d_table, c->d_issue, c->d_issue_n};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     dsm_text_release(c);
@@ -815,10 +889,19 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     if (grid_fb > 1024) grid_fb = 1024;
     uint64_t dblocks = (n_sys * np + 255) / 256;
     if (dblocks > (uint64_t)c->cus * 8) dblocks = (uint64_t)c->cus * 8;
+    /* two-pass schedule: the resume pass's partials follow the others (its grid is sized
+     * once the budget pass's suspended count is known) */
+    const uint32_t blog = (mode == 0 && !gen) ? budget_log2() : 0u;
     const size_t waves = (size_t)grid_fast * FW + (size_t)grid_fb + (size_t)dblocks;
+    const size_t waves_cap = waves + (blog ? (size_t)grid_fast * FW : 0);
     int rc;
-    if ((rc = ensure(&c->d_partials, &c->partials_waves, waves * K_N))) return rc;
+    if ((rc = ensure(&c->d_partials, &c->partials_waves, waves_cap * K_N))) return rc;
     if ((rc = ensure(&c->d_ovf_list, &c->ovf_cap, (size_t)n_sys))) return rc;
+    const int ring_eff = (mode && c->ring != 4) ? 12 : c->ring;   /* fast_mode's choice */
+    if (blog) {
+        if ((rc = ensure(&c->d_susp, &c->susp_cap, (size_t)n_sys * np * susp_words(ring_eff)))) return rc;
+        if ((rc = ensure(&c->d_susp_list, &c->susp_list_cap, (size_t)n_sys))) return rc;
+    }
     if ((rc = ensure(&c->d_recs, &c->recs_cap, (size_t)n_sys * np * 8))) return rc;
     if (!d_results) {   /* the engine needs the per-system header even if the caller does not */
         if ((rc = ensure(&c->d_res, &c->res_cap, (size_t)n_sys + 1))) return rc;
@@ -850,6 +933,11 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.table = c->d_table;
     A.sched_seed = c->sched_seed;
     A.sched_thresh = c->sched_thresh;
+    A.rsh = blog ? blog : RSH_MAX;
+    A.budget = blog ? 1u : 0u;
+    A.susp = c->d_susp;
+    A.susp_list = c->d_susp_list;
+    A.susp_count = c->d_ctrl + CTRL_SUSP;
     if (tr) {
         const size_t cap = (size_t)np * c->cfg.max_instr;
         if ((rc = ensure(&c->d_issue, &c->issue_cap_total, (size_t)n_sys * cap))) return rc;
@@ -867,12 +955,43 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     B.claim = c->d_ctrl + CTRL_FB;
     B.ovf_list = nullptr;
     B.ovf_count = nullptr;
+    B.rsh = RSH_MAX;
+    B.budget = 0;
     HIPCK(hipMemcpyAsync(c->d_args, c->h_args, 2 * sizeof(SimArgs), hipMemcpyHostToDevice, st));
     HIPCK(hipEventRecord(c->ev_args, st));
 
     if (c->ev0) HIPCK(hipEventRecord(c->ev0, st));
     hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, (const SimArgs *)c->d_args);
     HIPCK(hipGetLastError());
+    int grid_res = 0;
+    if (blog) {
+        /* resume pass: every suspended system continues; the grid holds an integral number
+         * of them per slot, so the slots (all running systems of similar remaining length)
+         * finish together */
+        uint32_t n_res = 0;
+        HIPCK(hipMemcpyAsync(&n_res, c->d_ctrl + CTRL_SUSP, sizeof n_res, hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+        if (n_res) {
+            const uint64_t slots_max = (uint64_t)grid_fast * FW * gpw;
+            const uint64_t per = (n_res + slots_max - 1) / slots_max;
+            const uint64_t slots = (n_res + per - 1) / per;
+            grid_res = (int)((slots + (uint64_t)(FW * gpw) - 1) / (uint64_t)(FW * gpw));
+            SimArgs &C = c->h_args[2];
+            C = A;
+            C.n_sys = n_res;
+            C.d_n = c->d_ctrl + CTRL_SUSP;
+            C.list = c->d_susp_list;
+            C.partials = c->d_partials + waves * K_N;
+            C.claim = c->d_ctrl + CTRL_RES;
+            C.rsh = RSH_MAX;
+            C.budget = 0;
+            C.resume = 1;
+            HIPCK(hipMemcpyAsync(c->d_args + 2, &C, sizeof(SimArgs), hipMemcpyHostToDevice, st));
+            HIPCK(hipEventRecord(c->ev_args, st));
+            hipLaunchKernelGGL(fast, dim3(grid_res), dim3(64 * FW), 0, st, (const SimArgs *)(c->d_args + 2));
+            HIPCK(hipGetLastError());
+        }
+    }
     if (c->ev1) { HIPCK(hipEventRecord(c->ev1, st)); c->timed = 1; }
 
     hipLaunchKernelGGL(fb, dim3(grid_fb), dim3(64), 0, st, (const SimArgs *)(c->d_args + 1));
@@ -887,15 +1006,17 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
                            (const uint4 *)c->d_recs, d_results, dpart);
     HIPCK(hipGetLastError());
 
-    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, st, c->d_partials, (int)waves,
-                       (unsigned long long *)d_counters);
+    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, st, c->d_partials,
+                       (int)(waves + (size_t)grid_res * FW), (unsigned long long *)d_counters);
     HIPCK(hipGetLastError());
 
     c->info.grid_blocks = grid_fast;
     c->info.block_threads = 64 * FW;
     c->info.waves_per_cu = nb_fast * FW;
     c->info.cus = c->cus;
-    c->info.ring_cap = (mode && c->ring != 4) ? 12 : c->ring;
+    c->info.ring_cap = ring_eff;
+    c->info.resume_blocks = grid_res;
+    c->info.budget_log2 = (int)blog;
     c->info.lds_bytes_per_block = lds_bytes(c->ring, FW);
     return DSM_OK;
 }

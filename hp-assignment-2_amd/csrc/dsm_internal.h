@@ -19,11 +19,15 @@ struct dsm_ctx {
     hipStream_t stream;
     int cus;
     unsigned int *d_ctrl;            /* claim shards (fast, fallback) + overflow count      */
-    SimArgs *d_args;                 /* [0] fast kernel, [1] 256-deep re-run                */
+    SimArgs *d_args;                 /* [0] fast kernel, [1] 256-deep re-run, [2] resume    */
     unsigned long long *d_partials;
     size_t partials_waves;
     uint32_t *d_ovf_list;
     size_t ovf_cap;
+    uint32_t *d_susp;                /* two-pass schedule: suspended node states             */
+    size_t susp_cap;
+    uint32_t *d_susp_list;           /*   and the suspended system ids                       */
+    size_t susp_list_cap;
     uint16_t *d_traces;
     size_t traces_cap;
     uint32_t *d_counts;

@@ -31,7 +31,7 @@ COUNTER_FIELDS = ([f"msgs_{t}" for t in TYPE_NAMES] +
                   ["msgs", "instrs", "rounds", "systems"] +
                   [f"status_{s}" for s in STATUS_NAMES] +
                   ["sum_dump_hash", "sum_final_hash", "max_rounds", "overflow_reruns",
-                   "wave_rounds"] + [f"reserved{i}" for i in range(5)])
+                   "wave_rounds", "resumed"] + [f"reserved{i}" for i in range(4)])
 assert len(COUNTER_FIELDS) == 32
 
 DUMP_BASE, DUMP_MAX, DUMP_SLOT = 1954, 1958, 1968
@@ -57,7 +57,8 @@ class Gen(ctypes.Structure):
 class LaunchInfo(ctypes.Structure):
     _fields_ = [("grid_blocks", ctypes.c_int), ("block_threads", ctypes.c_int),
                 ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int),
-                ("ring_cap", ctypes.c_int), ("lds_bytes_per_block", ctypes.c_int)]
+                ("ring_cap", ctypes.c_int), ("lds_bytes_per_block", ctypes.c_int),
+                ("resume_blocks", ctypes.c_int), ("budget_log2", ctypes.c_int)]
 
 
 _lib = None

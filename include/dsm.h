@@ -147,7 +147,8 @@ typedef struct dsm_counters {
     uint64_t max_rounds;       /* max, not sum */
     uint64_t overflow_reruns;  /* systems re-run with the 256-deep inbox */
     uint64_t wave_rounds;      /* lock-step loop iterations summed over waves (cost model) */
-    uint64_t reserved[5];
+    uint64_t resumed;          /* systems the two-pass schedule suspended and resumed      */
+    uint64_t reserved[4];
 } dsm_counters;
 
 typedef struct dsm_ctx dsm_ctx;
@@ -160,6 +161,8 @@ typedef struct dsm_launch_info {
     int cus;
     int ring_cap;
     int lds_bytes_per_block;
+    int resume_blocks;     /* two-pass schedule: workgroups of the resume pass (0: none)   */
+    int budget_log2;       /* its budget pass's round budget, log2 (0: one pass)          */
 } dsm_launch_info;
 
 /* ---- library ---------------------------------------------------------------------- */

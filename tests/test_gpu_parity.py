@@ -174,6 +174,39 @@ def test_device_entry_points_and_accumulation(dsm, orc):
     assert cd["max_rounds"] == int(ores["rounds"].max())
 
 
+@pytest.mark.parametrize("dist,ring,blog", [("uniform", 12, 5), ("hot", 12, 7), ("evict", 12, 3),
+                                             ("uniform", 4, 6), ("uniform", 8, 12)])
+def test_two_pass_schedule(dsm, orc, monkeypatch, dist, ring, blog):
+    """The packed path's two-pass schedule: a budget pass suspends every system still running
+    after 2^blog rounds (state to HBM), a resume pass continues it.  With tiny budgets almost
+    every system is suspended mid-flight (rings holding messages, waits pending, trace chunks
+    half consumed); results, records and counters must equal the oracle's single pass, and
+    overflow re-runs (ring 4) must compose with suspension."""
+    monkeypatch.setenv("DSM_BUDGET_LOG2", str(blog))
+    n = 4096
+    tr, cn = orc.generate(8, dist, 21, 4096, 777, n)
+    with dsm.Engine(8, 4096, ring_cap=ring, snapshots=True) as eng:
+        res, cnt = eng.run_packed(tr, cn)
+        info = eng.launch_info()
+        ores, obt, odump, ofin = orc.run_packed(8, tr, cn, records=True, nthreads=16)
+        for s in range(0, n, 97):
+            mask = int(ores[s]["status"]) >> 8
+            for nd in range(8):
+                d, f = eng.node_state(s, nd)
+                assert np.array_equal(f, ofin[s, nd])
+                if (mask >> nd) & 1:
+                    assert np.array_equal(d, odump[s, nd])
+    _cmp(res, ores)
+    assert info["budget_log2"] == blog
+    longer = int((ores["rounds"] >= (1 << blog)).sum())
+    assert cnt["resumed"] >= longer - cnt["overflow_reruns"] and cnt["resumed"] > 0
+    assert info["resume_blocks"] > 0
+    assert cnt["systems"] == n and cnt["msgs"] == int(ores["msgs"].sum())
+    assert cnt["sum_final_hash"] == int(ores["final_hash"].sum(dtype=np.uint64))
+    assert cnt["sum_dump_hash"] == int(ores["dump_hash"].sum(dtype=np.uint64))
+    assert cnt["max_rounds"] == int(ores["rounds"].max())
+
+
 def test_full_size_1m_random(dsm, orc):
     """C3 at full size: 1M 8-node systems, 4096 instructions per node, traces resident in
     HBM (64 GiB).  Per-system results of the HBM-trace path equal the fused-generator path
