@@ -281,15 +281,24 @@ def main():
         if args.fused:
             alg_bytes = 32 * local_c["systems"]
         ach = alg_bytes / (kavg * 1e-3) / 1e9
+        li = eng.launch_info()
+        # the packed path runs the transition kernel as two launches per step (budget pass +
+        # resume pass, run_engine's two-pass schedule): bytes and time are per step, i.e. the
+        # sum over both launches (rocprof lists 2 sim_kernel dispatches per step)
+        launches = 2 if li.get("resume_blocks") else 1
         roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
-                    kernel="sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel; 4-wave groups, ring 12, packed traces)",
+                    kernel="sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel; 4-wave groups, ring 12, packed traces)"
+                           + (f"; budget pass (2^{li['budget_log2']} rounds) + resume pass" if launches == 2 else ""),
+                    launches_per_step=launches,
                     algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),
-                    per_unit="2 B per consumed packed instruction + 32 B result + 4*np B counts per system")
+                    per_unit="2 B per consumed packed instruction + 32 B result + 4*np B counts per system"
+                             + ("; 'launch' = one step's budget + resume launches" if launches == 2 else ""))
         tr = traffic_from_profiles(args.config) or {}
         if tr.get("sim_kernel") and not args.fused:
-            roof["traffic"] = tr["sim_kernel"].get("bytes_per_launch")
-            roof["traffic_source"] = tr["sim_kernel"].get("source")
+            roof["traffic"] = int(tr["sim_kernel"].get("bytes_per_launch") * launches)
+            roof["traffic_source"] = tr["sim_kernel"].get("source") + (
+                " (per-dispatch average x 2 dispatches per step)" if launches == 2 else "")
         for phase, kname in ((trace_parse, "parse_kernel"), (dump_stream, "fmt_kernel"),
                              (trace_stream, "gen_kernel")):
             if phase is not None and tr.get(kname):
