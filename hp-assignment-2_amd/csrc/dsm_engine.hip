@@ -68,6 +68,7 @@ struct SimArgs {
     uint32_t rsh;                   /* round-limit test: rounds >> rsh != 0                  */
     uint32_t budget;                /* budget pass: suspend at 1 << rsh rounds               */
     uint32_t resume;                /* resume pass: start() restores a suspended system      */
+    uint32_t late_rsh;              /* budget pass: the budget once a wave finds no new work  */
     uint32_t *susp;                 /* [sys][word][node] suspended state (susp_words)        */
     uint32_t *susp_list;            /* budget pass: suspended system ids                     */
     unsigned int *susp_count;
@@ -247,7 +248,8 @@ sim_kernel(const SimArgs *Ap) {
     const uint64_t gfirst = GEN ? Ap->first_sys : 0;
     const int gdist = GEN ? Ap->dist : 0;
     const uint32_t stride = GEN ? 0u : Ap->stride;   /* >= 8, multiple of 8 (dsm_open) */
-    const uint32_t rsh = BUD ? Ap->rsh : RSH_MAX;
+    uint32_t rsh = BUD ? Ap->rsh : RSH_MAX;              /* wave-uniform (an SGPR) */
+    const uint32_t late_rsh = BUD ? Ap->late_rsh : 0u;
     const bool budget = BUD && Ap->budget != 0, resume = BUD && Ap->resume != 0;
 
     Node nd;
@@ -264,7 +266,9 @@ sim_kernel(const SimArgs *Ap) {
 
     /* initializeProcessor :778-790 and main :142-146 for a new system in this lane's group */
     auto start = [&](uint64_t s) {
-        sys = list ? (uint64_t)list[s] : s;
+        /* the resume pass takes its list last-suspended first: those were cut short by the
+         * late budget and may hold the most remaining rounds */
+        sys = list ? (uint64_t)list[resume ? n - 1 - s : s] : s;
         if (resume) {                 /* continue a system the budget pass suspended */
             const uint32_t *sp = Ap->susp + sys * (uint64_t)(SW * NP) + node;
 #pragma unroll
@@ -569,7 +573,12 @@ sim_kernel(const SimArgs *Ap) {
                 }
             }
         }
-        liveb = __ballot(live);
+        const uint64_t nlive = __ballot(live);
+        /* budget pass: once a slot of this wave found no new system, the wave's remaining
+         * systems get the late budget, so the launch's tail is not a system claimed last
+         * running its full budget at falling occupancy (the resume pass continues them) */
+        if (budget && late_rsh && (liveb & ~nlive)) rsh = late_rsh < rsh ? late_rsh : rsh;
+        liveb = nlive;
     }
 
     /* publish this wave's counters */
@@ -935,6 +944,11 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.sched_thresh = c->sched_thresh;
     A.rsh = blog ? blog : RSH_MAX;
     A.budget = blog ? 1u : 0u;
+    {
+        const char *e = getenv("DSM_LATE_LOG2");
+        const long v = (e && *e) ? strtol(e, nullptr, 10) : 10;
+        A.late_rsh = (blog && v > 0 && (uint32_t)v < blog) ? (uint32_t)v : 0u;
+    }
     A.susp = c->d_susp;
     A.susp_list = c->d_susp_list;
     A.susp_count = c->d_ctrl + CTRL_SUSP;
@@ -985,6 +999,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
             C.claim = c->d_ctrl + CTRL_RES;
             C.rsh = RSH_MAX;
             C.budget = 0;
+            C.late_rsh = 0;
             C.resume = 1;
             HIPCK(hipMemcpyAsync(c->d_args + 2, &C, sizeof(SimArgs), hipMemcpyHostToDevice, st));
             HIPCK(hipEventRecord(c->ev_args, st));
