@@ -396,7 +396,11 @@ sim_kernel(const SimArgs *Ap) {
         const uint32_t hdr = reinterpret_cast<const uint32_t *>(&s_tab[DT_ENTRIES])[opx];
         const uint32_t ti = dt_index(in, hdr, &evDb);
         const uint2 E = s_tab[ti];
-        const DtOut o = dt_apply(in, E.x, E.y, evDb);
+        /* dt_x / dt_y from the raw words: w = {v, a | x << 7, ..}, lw = {La, Lv, Ls, 0},
+         * mbw = {Mv, Db}, ctl = {pending, ..} */
+        const uint32_t X = __builtin_amdgcn_perm(lw, w, 0x05040001u) & ~0x80u;
+        const uint32_t Y = __builtin_amdgcn_perm(mbw, nd.ctl, 0x0C050400u) | ((evDb & 0xFFu) << 24);
+        const DtOut o = dt_apply_xy(in, X, Y, E.x, E.y, evDb);
         const uint32_t o0 = o.o0, o1 = o.o1;
 
         /* ---- (3) write back (idle lanes rewrite unchanged values) ------------------- */

@@ -397,12 +397,17 @@ DSM_HD uint32_t dt_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
 #endif
 }
 
-DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb) {
+/* the byte-permute operands: X = {a, v, La, Lv}, Y = {pending, Mv, Db, evDb} (the kernel
+ * assembles both from its raw words with two permutes, dt_apply_xy) */
+DSM_HD uint32_t dt_x(const DtIn &in) { return in.a | (in.v << 8) | (in.La << 16) | (in.Lv << 24); }
+DSM_HD uint32_t dt_y(const DtIn &in, uint32_t evDb) {
+    return in.pend | (in.Mv << 8) | (in.Db << 16) | ((evDb & 0xFFu) << 24);
+}
+
+DSM_HD DtOut dt_apply_xy(const DtIn &in, uint32_t X, uint32_t Y, uint32_t W0, uint32_t W1, uint32_t evDb) {
     DtOut o;
     const uint32_t H = in.a >> 4, sbit = 1u << in.s;
     /* the four byte results in one byte permute */
-    const uint32_t X = in.a | (in.v << 8) | (in.La << 16) | (in.Lv << 24);
-    const uint32_t Y = in.pend | (in.Mv << 8) | (in.Db << 16) | ((evDb & 0xFFu) << 24);
     const uint32_t P = dt_perm(Y, X, W0);
     o.P = P;
     o.nLa = P & 0xFFu;
@@ -444,6 +449,9 @@ DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb) {
     o.pendw = (W1 & W1_PEND) != 0u;
     o.asrt = (W1 & W1_ASSERT) != 0u;
     return o;
+}
+DSM_HD DtOut dt_apply(const DtIn &in, uint32_t W0, uint32_t W1, uint32_t evDb) {
+    return dt_apply_xy(in, dt_x(in), dt_y(in, evDb), W0, W1, evDb);
 }
 
 #endif
