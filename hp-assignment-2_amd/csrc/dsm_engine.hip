@@ -409,7 +409,7 @@ sim_kernel(const SimArgs *Ap) {
         *mbp = (uint16_t)(o.nMv | (o.nDb << 8));
         nd.ctl = (nd.ctl & ~o.cclr) | o.cset;      /* wait, pendingWriteValue (:633), assert */
         const bool isMsg = op <= T_EVM;
-        nd.nmsg += isMsg ? 1u : 0u;
+        if (FB) nd.nmsg += isMsg ? 1u : 0u;     /* else messages received, counted at delivery */
         if (TC) {
             const uint32_t inc = isMsg ? (1u << ((op & 1u) * 16)) : 0u, q = op >> 1;
 #pragma unroll
@@ -438,6 +438,12 @@ sim_kernel(const SimArgs *Ap) {
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         uint32_t R = s_rm[wv][lane];     /* bit 2*sender+word: that word is addressed to me */
         s_rm[wv][lane] = 0;
+        /* the fast kernel counts messages received (handled = received - still in the ring,
+         * taken at the finish); an overflow is flagged here and set in ctl on the finish
+         * path, where its system ends */
+        if (!FB)      /* one v_bcnt with its accumulator (the compiler would share the count) */
+            asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(nd.nmsg) : "v"(R));
+        uint32_t nccv;
         {
             /* appended at the tail in R's bit order.  An overflowing ring sets C_OVF and its
              * tail wraps onto live entries: the system ends this round (the transition
@@ -445,7 +451,7 @@ sim_kernel(const SimArgs *Ap) {
              * ring is not part of any record or result. */
             const uint32_t hh = nd.rh & 0xFFu, cc = nd.rh >> 8;
             const uint32_t ncc = cc + __builtin_popcount(R);
-            if (ncc > (uint32_t)RING) nd.ctl |= C_OVF;
+            nccv = ncc;
             uint32_t slot = hh + cc;
             slot = slot >= (uint32_t)RING ? slot - RING : slot;
             while (R) {
@@ -476,11 +482,13 @@ sim_kernel(const SimArgs *Ap) {
         asm volatile("" : "+v"(opv));
         const uint64_t actb = __ballot(opv != OP_IDLE || stall);   /* stalled = available */
         /* rounds >> rsh: DSM_MAX_ROUNDS, or the budget pass's 1 << rsh */
-        const uint64_t flagb = __ballot(((nd.ctl & (C_ASSERT | C_OVF)) | (rounds >> rsh)) != 0u);
+        const uint64_t flagb = __ballot(((nd.ctl & C_ASSERT) | (rounds >> rsh)) != 0u) |
+                               __ballot(nccv > (uint32_t)RING);
         constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
         constexpr uint64_t GHI = GLO << (NP - 1);
         const uint64_t t = actb | ~liveb;
         if ((((t - GLO) & ~t & GHI) | (flagb & liveb)) == 0) continue;
+        if (nccv > (uint32_t)RING) nd.ctl |= C_OVF;
         const uint32_t gact = (uint32_t)(actb >> gbase) & NPM;
         const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
         const bool gbad = ((badb >> gbase) & NPM) != 0;
@@ -518,7 +526,7 @@ sim_kernel(const SimArgs *Ap) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k) { q[(7 + k) * NP] = cur[k]; q[(11 + k) * NP] = nxt[k]; }
                 }
-                const uint32_t ins = gsum32<NP>(nd.ip), msgs = gsum32<NP>(nd.nmsg);
+                const uint32_t ins = gsum32<NP>(nd.ip), msgs = gsum32<NP>(nd.nmsg - (FB ? 0u : nd.rh >> 8));
                 uint32_t nlo = 0xFFFFFFFFu, nhi = 0xFFFFFFFFu;
                 if (node == 0) {
                     if (susp) {
