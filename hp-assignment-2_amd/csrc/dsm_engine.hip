@@ -392,8 +392,12 @@ sim_kernel(const SimArgs *Ap) {
         in.La = lw & 0xFFu; in.Lv = (lw >> 8) & 0xFFu; in.Ls = lw >> 16;
         in.Db = mbw >> 8; in.Ds = get2(nd.dst, blk); in.Mv = mbw & 0xFFu; in.pend = nd.ctl & 0xFFu;
         uint32_t evDb;
-        const uint32_t opx = dt_opx(in);
-        const uint32_t hdr = reinterpret_cast<const uint32_t *>(&s_tab[DT_ENTRIES])[opx];
+        /* header of op' = dt_opx(in): indexed by op | home << 5 (dt_build's second half
+         * maps EVICT_SHARED at its home to DT_EVSH); with fewer than 8 nodes an instruction
+         * whose home is not simulated is DT_ASSERT */
+        uint32_t hix = op | ((in.a >> 4) == node ? 32u : 0u);
+        if (NP < 8) hix = (op == DT_RD && (in.a >> 4) >= (uint32_t)NP) ? (uint32_t)DT_ASSERT : hix;
+        const uint32_t hdr = reinterpret_cast<const uint32_t *>(&s_tab[DT_ENTRIES])[hix];
         const uint32_t ti = dt_index(in, hdr, &evDb);
         const uint2 E = s_tab[ti];
         /* dt_x / dt_y from the raw words: w = {v, a | x << 7, ..}, lw = {La, Lv, Ls, 0},

@@ -50,8 +50,8 @@ enum : uint32_t {
     DT_WBINV = 7, DT_WBINT = 8, DT_FLUSH = 9, DT_FLINV = 10, DT_EVS = 11, DT_EVM = 12,
     DT_RD = 13, DT_WR = 14, DT_DUMP = 15, DT_IDLE = 16, DT_EVSH = 17, DT_ASSERT = 18,
     DT_NOPS = 20, DT_STRIDE = 32,
-    DT_ENTRIES = 320,                       /* row capacity (dt_build packs 268 rows)      */
-    DT_HDR_WORDS = 32, DT_TABLE_WORDS = 2 * DT_ENTRIES + DT_HDR_WORDS
+    DT_ENTRIES = 272,                       /* row capacity (dt_build packs 268 rows)      */
+    DT_HDR_WORDS = 64, DT_TABLE_WORDS = 2 * DT_ENTRIES + DT_HDR_WORDS
 };
 enum : uint32_t { DT_CM = 0, DT_CE = 1, DT_CS = 2, DT_CI = 3 };   /* cacheLineState :17 */
 enum : uint32_t { DT_DEM = 0, DT_DS = 1, DT_DU = 2 };             /* directoryEntryState :18 */
@@ -305,6 +305,11 @@ static inline uint32_t dt_build(uint32_t *tab) {
             if (row < DT_ENTRIES) dt_compile(e, h, &tab[2 * row], &tab[2 * row + 1]);
         }
     }
+    /* second half, indexed by op | 32 when the message's home is this node: the same
+     * headers, with EVICT_SHARED's at-home op (the kernel indexes the header by
+     * op | home << 5 instead of selecting DT_EVSH; dt_opx states the same choice) */
+    for (uint32_t op = 0; op < 32; ++op)
+        tab[2 * DT_ENTRIES + 32 + op] = tab[2 * DT_ENTRIES + (op == DT_EVS ? (uint32_t)DT_EVSH : op)];
     return row;                                  /* rows used; must not exceed DT_ENTRIES */
 }
 
