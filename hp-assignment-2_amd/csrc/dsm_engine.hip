@@ -686,8 +686,8 @@ __global__ void __launch_bounds__(256) digest_kernel(uint64_t n_sys, const uint4
  * non-temporal stores (written once, read later by another kernel). */
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int NP>
-__global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist, uint64_t first,
+template <int NP, int DIST, bool FULL>
+__global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist_unused, uint64_t first,
                                                   uint64_t n_sys, uint32_t n_instr,
                                                   uint32_t stride, uint16_t *traces,
                                                   uint32_t *counts) {
@@ -700,6 +700,8 @@ __global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist, uint6
         /* key = (sys << 16) | (node << 12) | (idx >> 2) -- disjoint fields, so + == | */
         const uint64_t base = gmul + ((first + sys) << 16) + ((uint64_t)node << 12);
         u32x4 *dst = reinterpret_cast<u32x4 *>(traces + slot * stride);
+        const int dist = DIST;
+#pragma unroll 2
         for (uint32_t k = threadIdx.x; k < cps; k += blockDim.x) {
             u32x4 v;
 #pragma unroll
@@ -709,9 +711,9 @@ __global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist, uint6
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const uint32_t ia = i0 + 2 * j;
-                    const uint32_t lo = (ia < n_instr)
+                    const uint32_t lo = (FULL || ia < n_instr)
                         ? instr_from_bits<NP>((uint32_t)(r >> (32 * j)) & 0xFFFFu, dist) : 0u;
-                    const uint32_t hi = (ia + 1 < n_instr)
+                    const uint32_t hi = (FULL || ia + 1 < n_instr)
                         ? instr_from_bits<NP>((uint32_t)(r >> (32 * j + 16)) & 0xFFFFu, dist) : 0u;
                     v[2 * half + j] = lo | (hi << 16);
                 }
@@ -1131,12 +1133,17 @@ extern "C" int dsm_generate_device(dsm_ctx *c, const dsm_gen *g, uint64_t first_
     uint64_t blocks = n_sys * (uint64_t)c->cfg.np;
     const uint64_t cap = (uint64_t)c->cus * 16;
     if (blocks > cap) blocks = cap;
-    if (c->cfg.np == 4)
-        hipLaunchKernelGGL(gen_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                           g->seed, g->dist, first_sys, n_sys, g->n_instr, c->cfg.max_instr, d_traces, d_counts);
-    else
-        hipLaunchKernelGGL(gen_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                           g->seed, g->dist, first_sys, n_sys, g->n_instr, c->cfg.max_instr, d_traces, d_counts);
+    /* the distribution and "every slot full" are compiled in (no per-instruction selects) */
+    const bool full = g->n_instr == c->cfg.max_instr;
+    const int np = c->cfg.np;
+    using gen_fn = void (*)(uint64_t, int, uint64_t, uint64_t, uint32_t, uint32_t, uint16_t *, uint32_t *);
+    static const gen_fn tab[2][3][2] = {
+        {{gen_kernel<4, 0, false>, gen_kernel<4, 0, true>}, {gen_kernel<4, 1, false>, gen_kernel<4, 1, true>},
+         {gen_kernel<4, 2, false>, gen_kernel<4, 2, true>}},
+        {{gen_kernel<8, 0, false>, gen_kernel<8, 0, true>}, {gen_kernel<8, 1, false>, gen_kernel<8, 1, true>},
+         {gen_kernel<8, 2, false>, gen_kernel<8, 2, true>}}};
+    hipLaunchKernelGGL(tab[np == 8][g->dist][full], dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       g->seed, g->dist, first_sys, n_sys, g->n_instr, c->cfg.max_instr, d_traces, d_counts);
     HIPCK(hipGetLastError());
     return DSM_OK;
 }
