@@ -1131,7 +1131,7 @@ extern "C" int dsm_generate_device(dsm_ctx *c, const dsm_gen *g, uint64_t first_
     if (n_sys == 0) return DSM_OK;
     HIPCK(hipSetDevice(c->device));
     uint64_t blocks = n_sys * (uint64_t)c->cfg.np;
-    const uint64_t cap = (uint64_t)c->cus * 16;
+    const uint64_t cap = (uint64_t)c->cus * 512;   /* many short-lived blocks: measured best (tools/ab_gen.sh) */
     if (blocks > cap) blocks = cap;
     /* the distribution and "every slot full" are compiled in (no per-instruction selects) */
     const bool full = g->n_instr == c->cfg.max_instr;

@@ -23,7 +23,7 @@ __device__ __forceinline__ uint64_t splitmix(uint64_t z) {
 template <int NP>
 __device__ __forceinline__ uint32_t instr_from_bits(uint32_t h, int dist) {
     const uint32_t wr = h & 1u;
-    const uint32_t val = wr ? (h >> 1) & 0xFFu : 0u;
+    const uint32_t val = (h >> 1) & (0u - wr) & 0xFFu;          /* RD: value 0 */
     const uint32_t sel = h >> 9;
     uint32_t addr;
     if (dist == DSM_DIST_HOT) addr = (sel & 3u) * 0x11u;
