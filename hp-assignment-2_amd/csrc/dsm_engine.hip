@@ -687,7 +687,7 @@ __global__ void __launch_bounds__(256) digest_kernel(uint64_t n_sys, const uint4
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <int NP, int DIST, bool FULL>
-__global__ void __launch_bounds__(256) gen_kernel(uint64_t seed, int dist_unused, uint64_t first,
+__global__ void __launch_bounds__(64) gen_kernel(uint64_t seed, int dist_unused, uint64_t first,
                                                   uint64_t n_sys, uint32_t n_instr,
                                                   uint32_t stride, uint16_t *traces,
                                                   uint32_t *counts) {
@@ -1142,7 +1142,7 @@ extern "C" int dsm_generate_device(dsm_ctx *c, const dsm_gen *g, uint64_t first_
          {gen_kernel<4, 2, false>, gen_kernel<4, 2, true>}},
         {{gen_kernel<8, 0, false>, gen_kernel<8, 0, true>}, {gen_kernel<8, 1, false>, gen_kernel<8, 1, true>},
          {gen_kernel<8, 2, false>, gen_kernel<8, 2, true>}}};
-    hipLaunchKernelGGL(tab[np == 8][g->dist][full], dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(tab[np == 8][g->dist][full], dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream,
                        g->seed, g->dist, first_sys, n_sys, g->n_instr, c->cfg.max_instr, d_traces, d_counts);
     HIPCK(hipGetLastError());
     return DSM_OK;
