@@ -13,10 +13,16 @@ the final RCCL all-reduce of the counters.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config random|hot|evict]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+With --gpus N > 1 and no torch.distributed launcher around it (WORLD_SIZE unset), the process
+starts N fresh rank processes itself (before anything touches the GPU), relays rank 0's JSON
+line and fails if any rank fails.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -61,6 +67,65 @@ def reduce_counters(vec, dist_mod=None):
     return vec
 
 
+def launch_ranks(n, argv, cmd=None, timeout=None):
+    """Start n rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT set; one GPU each by LOCAL_RANK) and wait for them.  Rank 0's stdout is
+    inherited (its JSON line is the result); the others' stdout is discarded.  When a rank
+    fails, the rest are terminated (by the PIDs started here) and its exit code returned.
+    `cmd` replaces [python, bench.py] (tests)."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    base = cmd or [sys.executable, os.path.abspath(__file__)]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(base + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    deadline = None if timeout is None else time.time() + timeout
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in pending:
+                    q.terminate()
+        if deadline is not None and time.time() > deadline and pending:
+            for q in pending:
+                q.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    return rc
+
+
+def host_cpu():
+    """The host's CPU as the baseline uses it: OpenMP threads (OMP_NUM_THREADS, else the
+    CPUs this process may run on), the machine's nproc and the CPU model."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = int(omp) if omp.isdigit() and int(omp) > 0 else aff
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return dict(threads=min(threads, aff), nproc=os.cpu_count(), affinity=aff, model=model,
+                omp_num_threads=omp or None)
+
+
 def cpu_baseline(dist, n_instr, seed, n_sample, threads):
     """The CPU oracle (clean-room C restatement, gcc -O2 -fopenmp, OpenMP over systems) on a
     bounded sample of the same system ids -- a reported baseline, not the target."""
@@ -74,7 +139,8 @@ def cpu_baseline(dist, n_instr, seed, n_sample, threads):
     msgs = int(res["msgs"].sum())
     return res, dict(value=msgs / dt, unit=UNIT, cores=threads, kind="port",
                      sample=f"systems 0..{n_sample - 1} of the same workload ({msgs} transactions,"
-                            f" {dt:.2f} s wall, {threads} OpenMP threads, traces generated lazily)")
+                            f" {dt:.2f} s wall, {threads} OpenMP threads, traces generated lazily)",
+                     msgs=msgs, instrs=int(res["instrs"].sum()))
 
 
 def cpu_baseline_reference(dist, n_instr, seed, n_sample, procs):
@@ -95,7 +161,7 @@ def cpu_baseline_reference(dist, n_instr, seed, n_sample, procs):
         return None
     d = json.loads(r.stdout.strip().splitlines()[-1])
     t = d["sim_ns_max"] * 1e-9
-    return dict(value=d["msgs"] / t, unit=UNIT, cores=procs, kind="reference",
+    return dict(value=d["msgs"] / t, unit=UNIT, cores=procs, kind="reference", msgs=d["msgs"],
                 sample=f"systems 0..{n_sample - 1} of the same workload ({d['msgs']} transactions); "
                        f"assignment.c's own handler/issue code (gcc -O2) under the lock-step "
                        f"schedule, {procs} processes, simulation time of the slowest "
@@ -123,13 +189,19 @@ def main():
     ap.add_argument("--ring", type=int, default=0)
     ap.add_argument("--fused", action="store_true",
                     help="generate instructions inside the transition kernel (no HBM traces)")
-    ap.add_argument("--cpu-sample", type=int, default=262144)
-    ap.add_argument("--cpu-ref-sample", type=int, default=65536)
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="systems for the port baseline (0: the whole workload)")
+    ap.add_argument("--cpu-ref-sample", type=int, default=0,
+                    help="systems for the reference baseline (0: the whole workload)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dump", action="store_true", help="skip the GPU dump-formatter phase")
     ap.add_argument("--parse-systems", type=int, default=65536,
                     help="systems whose core files are generated as text and GPU-parsed (0: skip)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one fresh process per GPU, started before this process touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -138,10 +210,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus <= 1):
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # test knobs (tests/test_gpu_bench.py): every rank on one device, gloo for the counters
+    if os.environ.get("DSM_BENCH_DEVICE"):
+        local = int(os.environ["DSM_BENCH_DEVICE"])
+    backend = os.environ.get("DSM_BENCH_BACKEND", "nccl")     # nccl = RCCL over xGMI
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 
@@ -189,18 +270,19 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    kms = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        kms.append(eng.last_kernel_ms())
+        step()          # asynchronous: the steps queue back to back on the stream
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the transition kernel's device time per step (HIP events around its launches, on the
+    # stream they run on), read after the timed region
+    kms = eng.kernel_ms_history(min(args.steps, 64))
 
     # initializeProcessor's reader on the GPU (parse_kernel): the same workload's core files as
     # text (shipped-test format) for the first --parse-systems systems, scanned back into packed
@@ -265,12 +347,13 @@ def main():
                            frac=round(fbytes / fms / 1e6 / HBM_PEAK_GBS, 4))
         del d_txt, d_len
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    cdev = dev if backend == "nccl" else torch.device("cpu")    # gloo: host tensors
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed_max = float(el.item())
     local_c = pydsm.counters_to_dict(cnt.cpu().numpy().view(np.uint64))
-    tot = reduce_counters(cnt.clone(), dist if world > 1 else None)
+    tot = reduce_counters(cnt.clone().to(cdev), dist if world > 1 else None)
     c = pydsm.counters_to_dict(tot.cpu().numpy().view(np.uint64))
 
     if rank == 0:
@@ -313,12 +396,17 @@ def main():
             parity = "golden[0:4096] bit-exact" if np.array_equal(mine, g) else "GOLDEN MISMATCH"
         cpu = cpu_port = None
         if world == 1 and not args.no_cpu:
-            threads = min(16, os.cpu_count() or 1)     # the GPU box's host share is 16 cores
-            cpu = cpu_baseline_reference(dname, n_instr, seed, min(args.cpu_ref_sample, n_sys),
-                                         threads)
-            _, cpu_port = cpu_baseline(dname, n_instr, seed, min(args.cpu_sample, n_sys), threads)
+            hc = host_cpu()
+            threads = hc["threads"]
+            cpu = cpu_baseline_reference(dname, n_instr, seed,
+                                         min(args.cpu_ref_sample or n_sys, n_sys), threads)
+            _, cpu_port = cpu_baseline(dname, n_instr, seed, min(args.cpu_sample or n_sys, n_sys),
+                                       threads)
             if cpu is None:
                 cpu, cpu_port = cpu_port, None
+            for b in (cpu, cpu_port):
+                if b is not None:
+                    b["host"] = hc
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": UNIT, "n_gpus": world,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed_max / K * 1e3, 3),
@@ -338,8 +426,10 @@ def main():
             "systems_per_s": round(c["systems"] * K / elapsed_max, 1),
             "instructions_per_s": round(c["instrs"] * K / elapsed_max, 1),
             "counters": {k: c[k] for k in ("msgs", "instrs", "rounds", "systems", "max_rounds",
-                                           "overflow_reruns", "wave_rounds", "status_COMPLETED",
+                                           "overflow_reruns", "wave_rounds", "resumed",
+                                           "ff_passes", "ff_steps", "status_COMPLETED",
                                            "status_DEADLOCKED")},
+            "kernel_ms": [round(x, 3) for x in kms],
             "sum_final_hash": hex(c["sum_final_hash"]),
             "parity": parity,
             "launch": eng.launch_info(),

@@ -53,7 +53,8 @@ struct SimArgs {
     int dist;
     dsm_sys_result *results;    /* the transition kernel writes the first 16 bytes        */
     uint4 *recs;                /* [sys][node][2] x 64 B: dump record, final record       */
-    unsigned long long *partials;   /* [waves][K_N], written once per wave at exit         */
+    unsigned long long *counters;   /* dsm_counters (device), accumulated into by atomics at
+                                     * workgroup exit (integer sums: order-independent)   */
     unsigned int *claim;            /* 8 shard counters, 32 words apart                     */
     uint32_t *ovf_list;             /* fast kernel: systems handed to the 256-deep re-run   */
     unsigned int *ovf_count;
@@ -72,7 +73,14 @@ struct SimArgs {
     uint32_t *susp;                 /* [sys][word][node] suspended state (susp_words)        */
     uint32_t *susp_list;            /* budget pass: suspended system ids                     */
     unsigned int *susp_count;
+    uint32_t lim_rsh;               /* round limit = 1 << lim_rsh (DSM_MAX_ROUNDS, or
+                                     * dsm_set_round_limit): ROUND_LIMIT at that many rounds */
+    uint32_t icap;                  /* inbox limit (MSG_BUFFER_SIZE = 256, or
+                                     * dsm_set_inbox_limit): RING_OVERFLOW beyond it        */
 };
+/* the argument blocks of one run, written to device memory by args_kernel (stream-ordered:
+ * no pinned staging whose reuse would need a host wait) */
+struct SimArgsPack { SimArgs a[3]; };
 
 
 #define DEVI __device__ __forceinline__
@@ -93,7 +101,8 @@ constexpr uint32_t C_WAIT = DT_CTL_WAIT, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C
 
 /* counter slots (dsm_counters order) */
 enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
-       K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_RESUMED = 27, K_N = 32 };
+       K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_RESUMED = 27,
+       K_FFPASS = 28, K_FFITER = 29, K_N = 32 };
 constexpr uint32_t RSH_MAX = 22;    /* 1 << 22 == DSM_MAX_ROUNDS */
 static_assert((1u << RSH_MAX) == DSM_MAX_ROUNDS, "DSM_MAX_ROUNDS");
 /* suspended node state: memory/bitVector (8), lines (4), ring (RING), dst, ctl, ip, nins, rh,
@@ -198,6 +207,68 @@ DEVI uint4 ld16(const uint16_t *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+/* ---- hit-run fast-forward helpers ------------------------------------------------------
+ * A trace chunk is 8 packed instructions in 4 dwords (instruction j = half-word j).       */
+/* the 8 instructions starting at half-word s (0..7) of the 16 in (a, b): low 128 bits of
+ * (b:a) >> 16 s.  Dword select (3 v_cndmask each) then one v_alignbit per output dword. */
+DEVI void ff_window(const uint32_t (&a)[4], const uint32_t (&b)[4], uint32_t s, uint32_t (&w)[4]) {
+    const uint32_t q = s >> 1, hs = (s & 1u) << 4;
+    const uint32_t d[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    uint32_t t[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        t[j] = q == 0 ? d[j] : q == 1 ? d[j + 1] : q == 2 ? d[j + 2] : d[j + 3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_alignbit(t[j + 1], t[j], hs);
+}
+/* x << 16 s (128 bits, zero fill): puts the shift register `cur` (instruction ip at its low
+ * half-word) back at its aligned position ip & 7 */
+DEVI void ff_unshift(const uint32_t (&x)[4], uint32_t s, uint32_t (&y)[4]) {
+    const uint32_t q = s >> 1;
+    const bool odd = s & 1u;
+    const uint32_t xz[7] = {0u, 0u, 0u, x[0], x[1], x[2], x[3]};   /* xz[3 + i] = x[i] */
+    uint32_t u[5];                                                 /* u[j + 1] = (x << 32 q)[j] */
+#pragma unroll
+    for (int j = -1; j < 4; ++j)
+        u[j + 1] = j < 0 ? 0u : q == 0 ? xz[3 + j] : q == 1 ? xz[2 + j] : q == 2 ? xz[1 + j] : xz[j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = odd ? __builtin_amdgcn_alignbit(u[j + 1], u[j], 16) : u[j + 1];
+}
+/* x >> 16 s (128 bits, zero fill): the shift-register form of an aligned chunk at ip & 7 = s */
+DEVI void ff_shift(const uint32_t (&x)[4], uint32_t s, uint32_t (&y)[4]) {
+    const uint32_t z[4] = {0u, 0u, 0u, 0u};
+    ff_window(x, z, s, y);
+}
+/* GEN: aligned chunk c (instructions 8c .. 8c+7) of the counter-based generator, in the
+ * packed-trace layout (gen_instr's key and bit fields) */
+template <int NP>
+DEVI void gen_chunk(uint64_t gmul, int dist, uint64_t sysg, uint32_t node, uint32_t c,
+                    uint32_t (&w)[4]) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const uint32_t i0 = (c * 8u + 4u * half) & 0xFFFu;
+        const uint64_t r = splitmix(gmul + ((sysg << 16) | ((uint64_t)node << 12) | (uint64_t)(i0 >> 2)));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            w[2 * half + j] = instr_from_bits<NP>((uint32_t)(r >> (32 * j)) & 0xFFFFu, dist) |
+                              (instr_from_bits<NP>((uint32_t)(r >> (32 * j + 16)) & 0xFFFFu, dist) << 16);
+    }
+}
+/* minimum over the NP lanes of a node group (all of them active): DPP quad swaps, then the
+ * half-row mirror for 8-lane groups */
+template <int NP>
+DEVI uint32_t gmin(uint32_t x) {
+    uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0xB1, 0xF, 0xF, false);
+    x = y < x ? y : x;
+    y = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x4E, 0xF, 0xF, false);
+    x = y < x ? y : x;
+    if (NP == 8) {
+        y = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x141, 0xF, 0xF, false);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
 
 /* ---- the transition kernel ------------------------------------------------------------ *
  * One loop iteration = one lock-step round of every system resident in the wave.  The 13
@@ -222,6 +293,9 @@ sim_kernel(const SimArgs *Ap) {
     constexpr bool FB = (RING == FB_RING);   /* the 256-deep re-run kernel                */
     constexpr bool TC = (MODE & M_TC) != 0, TR = (MODE & M_TR) != 0, SX = (MODE & M_SX) != 0;
     constexpr bool BUD = MODE == 0 && !FB && !GEN;   /* the two-pass schedule's suspend/resume */
+    /* hit-run fast-forward: wherever the order of issues inside a round is not observed
+     * (not with the issue-order trace or the seeded stalls of schedule exploration) */
+    constexpr bool FF = (MODE & (M_TR | M_SX)) == 0;
     constexpr int SW = susp_words(RING);
 
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
@@ -248,14 +322,32 @@ sim_kernel(const SimArgs *Ap) {
     const uint64_t gfirst = GEN ? Ap->first_sys : 0;
     const int gdist = GEN ? Ap->dist : 0;
     const uint32_t stride = GEN ? 0u : Ap->stride;   /* >= 8, multiple of 8 (dsm_open) */
-    uint32_t rsh = BUD ? Ap->rsh : RSH_MAX;              /* wave-uniform (an SGPR) */
+    const uint32_t lim_rsh = Ap->lim_rsh;                /* round limit 1 << lim_rsh       */
+    const uint32_t lim = 1u << lim_rsh;
+    /* an inbox beyond ocap ends the round's system: the fast kernel hands it to the 256-deep
+     * re-run (its ring holds RING), which reports RING_OVERFLOW beyond the inbox limit */
+    const uint32_t ocap = FB || Ap->icap < (uint32_t)RING ? Ap->icap : (uint32_t)RING;
+    uint32_t rsh = BUD && Ap->rsh < lim_rsh ? Ap->rsh : lim_rsh;   /* wave-uniform (an SGPR) */
     const uint32_t late_rsh = BUD ? Ap->late_rsh : 0u;
     const bool budget = BUD && Ap->budget != 0, resume = BUD && Ap->resume != 0;
+    /* systems started statically (one per slot), the rest claimed from the shard counters.
+     * The resume pass is launched at the full grid and sizes itself here from the device-
+     * resident count of suspended systems (no host round trip): it uses the fewest slots
+     * that hold an equal whole number of them, so the slots (all running systems of similar
+     * remaining length) finish together; the other slots exit at once. */
+    uint64_t pool = (uint64_t)gridDim.x * WAVES * GPW;
+    if (resume && n) {
+        const uint64_t per = (n + pool - 1) / pool;
+        pool = (n + per - 1) / per;
+    }
 
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
-    const uint16_t *tb = nullptr;
     uint64_t sys = 0;
+    /* this node's trace slot, recomputed where used (a per-lane 64-bit pointer kept across
+     * the round loop would push the kernel over its VGPR budget) */
+    const uint16_t *const traces = Ap->traces;
+    auto tslot = [&]() { return traces + (sys * NP + node) * (uint64_t)stride; };
     uint32_t rounds = 0, rmsg = 0;
     bool live = false;
     uint32_t tc[7] = {0, 0, 0, 0, 0, 0, 0};                                  /* TC only */
@@ -282,13 +374,16 @@ sim_kernel(const SimArgs *Ap) {
             nd.rh = q[4 * NP]; nd.nmsg = q[5 * NP]; rounds = q[6 * NP];
 #pragma unroll
             for (int k = 0; k < 4; ++k) { cur[k] = q[(7 + k) * NP]; nxt[k] = q[(11 + k) * NP]; }
-            tb = Ap->traces + (sys * NP + node) * (uint64_t)stride;
             rmsg = s_ring[wv][nd.rh & 0xFFu][lane];          /* the head, as the loop keeps it */
             return;
         }
+        /* an opaque copy of the node id: keeps these per-system constants from being
+         * hoisted out of the round loop, where they would only take registers */
+        uint32_t nn = node;
+        asm volatile("" : "+v"(nn));
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            s_mb[wv][i][lane] = ((20u * node + 2 * i) & 0xFFu) | (((20u * node + 2 * i + 1) & 0xFFu) << 16);
+            s_mb[wv][i][lane] = ((20u * nn + 2 * i) & 0xFFu) | (((20u * nn + 2 * i + 1) & 0xFFu) << 16);
         nd.dst = 0xAAAAAAAAu;
 #pragma unroll
         for (int i = 0; i < 4; ++i) s_line[wv][i][lane] = DSM_LINE_INIT;
@@ -304,7 +399,7 @@ sim_kernel(const SimArgs *Ap) {
         } else {
             const uint32_t c = Ap->counts[sys * NP + node];
             nd.nins = c < stride ? c : stride;
-            tb = Ap->traces + (sys * NP + node) * (uint64_t)stride;
+            const uint16_t *tb = tslot();
             /* both chunks unconditionally (in-slot), then drain them here, once per system:
              * the round loop's only vmcnt wait is then the refill rotation */
             const uint4 v0 = ld16(tb), v1 = ld16(tb + (stride > 8 ? 8 : 0));
@@ -314,7 +409,7 @@ sim_kernel(const SimArgs *Ap) {
         }
     };
 
-    if (G < n) {
+    if (G < n && G < pool) {
         live = true;
         start(G);
     } else {
@@ -322,6 +417,7 @@ sim_kernel(const SimArgs *Ap) {
     }
 
     uint32_t wrounds = 0;    /* loop iterations of this wave (uniform) */
+    uint32_t ffpass = 0, ffiter = 0;   /* fast-forward passes / steps of this wave (uniform) */
     uint64_t liveb = __ballot(live);
     for (;;) {
         if (liveb == 0) break;
@@ -354,7 +450,7 @@ sim_kernel(const SimArgs *Ap) {
          * same basic block stalls the whole wave on HBM). */
         const bool refill = !GEN && doIssue && ((nd.ip + 1) & 7u) == 0 && nd.ip + 1 < nd.nins;
         uint4 pf;
-        if (refill) pf = ld16(tb + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
+        if (refill) pf = ld16(tslot() + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
         const uint32_t headn = (head0 + 1 == (uint32_t)RING) ? 0u : head0 + 1;
         nd.rh = hasMsg ? (headn | ((cnt0 - 1) << 8)) : nd.rh;
         uint32_t w = rmsg;
@@ -434,10 +530,13 @@ sim_kernel(const SimArgs *Ap) {
          * group's destination bytes */
         {
             uint32_t m0 = o0 >> 24, m1 = o1 >> 24;
-            if (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], 1u << (2 * node)); m0 &= m0 - 1; }
-            if (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], 2u << (2 * node)); m1 &= m1 - 1; }
-            while (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], 1u << (2 * node)); m0 &= m0 - 1; }
-            while (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], 2u << (2 * node)); m1 &= m1 - 1; }
+            uint32_t b0 = 2 * node;            /* recomputed here, not kept in a register */
+            asm volatile("" : "+v"(b0));
+            const uint32_t bit0 = 1u << b0, bit1 = 2u << b0;
+            if (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
+            if (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
+            while (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
+            while (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         uint32_t R = s_rm[wv][lane];     /* bit 2*sender+word: that word is addressed to me */
@@ -474,6 +573,128 @@ sim_kernel(const SimArgs *Ap) {
             nxt[0] = pf.x; nxt[1] = pf.y; nxt[2] = pf.z; nxt[3] = pf.w;
         }
 
+        /* ---- (4b) hit-run fast-forward (exact) ----------------------------------------- *
+         * After a round in which a system sent nothing (every node issued a hit -- RD hit,
+         * :607-611; WR hit on M/E, :635-645 -- or idled), every inbox of it is empty, and
+         * until some node issues an instruction that sends, nothing reaches any node: each
+         * round is then one more local hit per non-waiting node (a waiting node stays idle,
+         * :578-581).  A hit never changes which later instructions hit (only E -> M, and
+         * values), so each issuing node's run of hits is fixed by its trace and its 4 line
+         * tags.  The group applies the next k rounds at once, k = the minimum run over its
+         * issuing nodes, 8 instructions per step: per node the last value written to each
+         * line (state M), pendingWriteValue (:633) and the instruction index, and
+         * rounds += k.  A node with instructions left but not yet dumped, or the round
+         * limit, bounds k; the round that breaks the run runs normally. */
+        if (FF) {
+            const bool quiet = (op == OP_RD || op == OP_IDLE) &&
+                               (((o0 | o1) >> 24) | (nd.ctl & C_ASSERT)) == 0u;
+            const uint64_t hitb = __ballot(quiet && op == OP_RD);
+            if (hitb) {
+                const uint64_t qb = __ballot(quiet);
+                const bool ffa = live && ((qb >> gbase) & NPM) == NPM && ((hitb >> gbase) & NPM) != 0;
+                if (__ballot(ffa)) {
+                    ++ffpass;
+                    const bool iss = ffa && (nd.ctl & C_WAIT) == 0u && nd.ip < nd.nins;
+                    const bool dpend = ffa && (nd.ctl & (C_WAIT | C_DUMPED)) == 0u && nd.ip >= nd.nins;
+                    /* line tags for a hit: RD needs a valid line, WR a line in M or E */
+                    uint32_t kr = 0, kw = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t lw = s_line[wv][i][lane];
+                        const uint32_t la = lw & 0xFFu, ls = lw >> 16;
+                        kr |= (ls != DT_CI ? la : 0xFFu) << (8 * i);
+                        kw |= (ls <= DT_CE ? la : 0xFFu) << (8 * i);
+                    }
+                    uint32_t A[4], B[4], P[4] = {0u, 0u, 0u, 0u};
+                    if (GEN) {
+                        gen_chunk<NP>(gmul, gdist, gfirst + sys, node, nd.ip >> 3, A);
+                        gen_chunk<NP>(gmul, gdist, gfirst + sys, node, (nd.ip >> 3) + 1, B);
+                    } else {
+                        ff_unshift(cur, nd.ip & 7u, A);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) B[q] = nxt[q];
+                    }
+                    /* little state across the loop (the kernel runs at its VGPR budget):
+                     * the window's aligned chunks A, B and the prefetch P, the line tags,
+                     * the values written per line; ip, pendingWriteValue and rounds are
+                     * updated in place */
+                    uint32_t lval = 0, wm = 0;
+                    bool act = ffa;
+                    for (;;) {
+                        if (__ballot(act) == 0) break;
+                        ++ffiter;
+                        if (act) {
+                            const uint32_t c = nd.ip >> 3, s = nd.ip & 7u;
+                            if (iss) {          /* next chunk in flight during the scan */
+                                if (GEN) {
+                                    gen_chunk<NP>(gmul, gdist, gfirst + sys, node, c + 2, P);
+                                } else {
+                                    const uint32_t pc = (c + 2) * 8u + 8u <= stride ? (c + 2) * 8u : stride - 8u;
+                                    const uint4 v = ld16(tslot() + pc);
+                                    P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
+                                }
+                            }
+                            uint32_t W[4];
+                            ff_window(A, B, s, W);
+                            uint32_t hm = 0;
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                const uint32_t h = (W[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                                const uint32_t key = (h & 0x8000u) ? kw : kr;
+                                const uint32_t tag = __builtin_amdgcn_ubfe(key, (h >> 5) & 0x18u, 8);
+                                hm |= (tag == ((h >> 8) & 0x7Fu)) ? (1u << j) : 0u;
+                            }
+                            uint32_t r = iss ? (uint32_t)__builtin_ctz(~hm) : (dpend ? 0u : 8u);
+                            if (iss && r > nd.nins - nd.ip) r = nd.nins - nd.ip;
+                            const uint32_t left = lim - 1u - rounds;   /* round limit */
+                            if (r > left) r = left;
+                            const uint32_t k = gmin<NP>(r);
+                            if (iss) {
+#pragma unroll
+                                for (int j = 0; j < 8; ++j) {
+                                    const uint32_t h = (W[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                                    if ((uint32_t)j < k && (h & 0x8000u)) {   /* WR hit :633, :640-645 */
+                                        const uint32_t sh = (h >> 5) & 0x18u;
+                                        lval = (lval & ~(0xFFu << sh)) | ((h & 0xFFu) << sh);
+                                        wm |= 1u << (sh >> 3);
+                                        nd.ctl = (nd.ctl & ~0xFFu) | (h & 0xFFu);
+                                    }
+                                }
+                                nd.ip += k;
+                            }
+                            rounds += k;
+                            if (k < 8u) {
+                                act = false;
+                                if (!GEN) {
+                                    /* shift register and next chunk at the (new) ip, rebuilt
+                                     * from the window's chunks (a node that did not issue gets
+                                     * its own back), so cur / nxt are dead across the loop */
+                                    const bool cross = s + (iss ? k : 0u) >= 8u;
+                                    uint32_t X[4];
+#pragma unroll
+                                    for (int q = 0; q < 4; ++q) X[q] = cross ? B[q] : A[q];
+                                    ff_shift(X, nd.ip & 7u, cur);
+#pragma unroll
+                                    for (int q = 0; q < 4; ++q) nxt[q] = cross ? P[q] : B[q];
+                                }
+                            } else if (iss) {      /* the others keep their chunks */
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) { A[q] = B[q]; B[q] = P[q]; }
+                            }
+                        }
+                    }
+                    if (iss) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if ((wm >> i) & 1u) {   /* value written, state MODIFIED (0) */
+                                const uint32_t lw = s_line[wv][i][lane];
+                                s_line[wv][i][lane] = (lw & 0xFFu) | (((lval >> (8 * i)) & 0xFFu) << 8);
+                            }
+                    }
+                }
+            }
+        }
+
         /* ---- (5) per-system termination (Appendix A step 4) -------------------------- *
          * A round in which no node of a system acts changes nothing, so every later round
          * is idle too: the active rounds of a system are a prefix, and `rounds` counts every
@@ -481,25 +702,25 @@ sim_kernel(const SimArgs *Ap) {
          * with no active lane (a zero field in actb | ~liveb), or a lane with an assert, an
          * overflow or the round limit; the per-lane finish runs only then. */
         ++rounds;
-        /* both tests on VGPR integers (one compare each; DSM_MAX_ROUNDS is a power of two) */
+        /* both tests on VGPR integers (one compare each; the round limit is a power of two) */
         uint32_t opv = op;
         asm volatile("" : "+v"(opv));
         const uint64_t actb = __ballot(opv != OP_IDLE || stall);   /* stalled = available */
-        /* rounds >> rsh: DSM_MAX_ROUNDS, or the budget pass's 1 << rsh */
+        /* rounds >> rsh: the round limit, or the budget pass's 1 << rsh */
         const uint64_t flagb = __ballot(((nd.ctl & C_ASSERT) | (rounds >> rsh)) != 0u) |
-                               __ballot(nccv > (uint32_t)RING);
+                               __ballot(nccv > ocap);
         constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
         constexpr uint64_t GHI = GLO << (NP - 1);
         const uint64_t t = actb | ~liveb;
         if ((((t - GLO) & ~t & GHI) | (flagb & liveb)) == 0) continue;
-        if (nccv > (uint32_t)RING) nd.ctl |= C_OVF;
+        if (nccv > ocap) nd.ctl |= C_OVF;
         const uint32_t gact = (uint32_t)(actb >> gbase) & NPM;
         const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
         const bool gbad = ((badb >> gbase) & NPM) != 0;
         if (gact == 0) --rounds;
         /* budget pass: a system still running after 1 << rsh rounds is suspended */
-        const bool susp = budget && gact != 0 && !gbad && rounds >= (1u << rsh);
-        const bool done = live && (gact == 0 || gbad || rounds >= DSM_MAX_ROUNDS || susp);
+        const bool susp = budget && gact != 0 && !gbad && rounds >= (1u << rsh) && rounds < lim;
+        const bool done = live && (gact == 0 || gbad || rounds >= lim || susp);
 
         const uint64_t doneb = __ballot(done);
         if (doneb) {
@@ -553,7 +774,6 @@ sim_kernel(const SimArgs *Ap) {
                         atomicMax(&s_cnt[wv][K_MAXR], (unsigned long long)rounds);
                     }
                     /* next system: static first assignment, then 8 sharded counters */
-                    const uint64_t pool = (uint64_t)gridDim.x * WAVES * GPW;
                     const uint64_t rs = n > pool ? (n - pool + 7) / 8 : 0;
                     while (tried < 8) {
                         const uint64_t lo = pool + (uint64_t)shard * rs;
@@ -597,28 +817,26 @@ sim_kernel(const SimArgs *Ap) {
         liveb = nlive;
     }
 
-    /* publish this wave's counters */
-    if (lane == 0) s_cnt[wv][K_WROUNDS] = wrounds;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (lane < K_N)
-        Ap->partials[((uint64_t)blockIdx.x * WAVES + wv) * K_N + lane] = s_cnt[wv][lane];
-}
-
-/* ---- partial-counter reduction (deterministic, one block) ---------------------------- */
-__global__ void __launch_bounds__(256) reduce_kernel(const unsigned long long *partials,
-                                                     int nwaves, unsigned long long *out) {
-    __shared__ unsigned long long s[8][K_N];
-    const int k = threadIdx.x & 31, r = threadIdx.x >> 5;
-    unsigned long long acc = 0;
-    for (int wv = r; wv < nwaves; wv += 8) {
-        const unsigned long long x = partials[(size_t)wv * K_N + k];
-        acc = (k == K_MAXR) ? (x > acc ? x : acc) : acc + x;
+    /* publish the workgroup's counters: its waves' rows summed in LDS, then one device-scope
+     * atomic per non-zero counter (integer sums mod 2^64 and a max: the result does not
+     * depend on the order, so no separate reduction pass is needed) */
+    if (lane == 0) {
+        s_cnt[wv][K_WROUNDS] = wrounds;
+        s_cnt[wv][K_FFPASS] = ffpass;
+        s_cnt[wv][K_FFITER] = ffiter;
     }
-    s[r][k] = acc;
     __syncthreads();
-    if (r == 0) {
-        for (int i = 1; i < 8; ++i) acc = (k == K_MAXR) ? (s[i][k] > acc ? s[i][k] : acc) : acc + s[i][k];
-        out[k] = (k == K_MAXR) ? (acc > out[k] ? acc : out[k]) : out[k] + acc;
+    if (threadIdx.x < K_N) {
+        unsigned long long v = s_cnt[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) {
+            const unsigned long long x = s_cnt[w][threadIdx.x];
+            v = threadIdx.x == K_MAXR ? (x > v ? x : v) : v + x;
+        }
+        if (v) {
+            if (threadIdx.x == K_MAXR) atomicMax(&Ap->counters[K_MAXR], v);
+            else atomicAdd(&Ap->counters[threadIdx.x], v);
+        }
     }
 }
 
@@ -629,7 +847,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(const unsigned long long *p
 template <int NP>
 __global__ void __launch_bounds__(256) digest_kernel(uint64_t n_sys, const uint4 *recs,
                                                      dsm_sys_result *results,
-                                                     unsigned long long *partials) {
+                                                     unsigned long long *counters) {
     __shared__ unsigned long long s_sum[2][4];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, node = lane % NP;
     uint64_t adh = 0, afh = 0;
@@ -672,11 +890,10 @@ __global__ void __launch_bounds__(256) digest_kernel(uint64_t n_sys, const uint4
     }
     if (lane == 0) { s_sum[0][wv] = adh; s_sum[1][wv] = afh; }
     __syncthreads();
-    if (threadIdx.x < K_N) {
-        unsigned long long v = 0;
-        if (threadIdx.x == K_DHASH) v = s_sum[0][0] + s_sum[0][1] + s_sum[0][2] + s_sum[0][3];
-        if (threadIdx.x == K_FHASH) v = s_sum[1][0] + s_sum[1][1] + s_sum[1][2] + s_sum[1][3];
-        partials[(uint64_t)blockIdx.x * K_N + threadIdx.x] = v;
+    if (threadIdx.x < 2) {      /* block sums into the counters (sums mod 2^64) */
+        const unsigned long long v = s_sum[threadIdx.x][0] + s_sum[threadIdx.x][1] +
+                                     s_sum[threadIdx.x][2] + s_sum[threadIdx.x][3];
+        if (v) atomicAdd(&counters[threadIdx.x ? K_FHASH : K_DHASH], v);
     }
 }
 
@@ -783,6 +1000,16 @@ int lds_bytes(int ring, int waves) {
     return waves * (8 * 64 * 4 + 4 * 64 * 4 + ring * 64 * 4 + 128 * 4 + 64 * 4 + K_N * 8) + DT_TABLE_WORDS * 4;
 }
 
+/* writes a run's argument blocks (passed by value in the kernarg segment) to device memory,
+ * in stream order: no pinned staging buffer, so nothing for the host to wait on */
+__global__ void __launch_bounds__(64) args_kernel(SimArgsPack p, SimArgs *dst) {
+    constexpr int W = (int)(sizeof(SimArgsPack) / 4);
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(&p);
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+    for (int i = threadIdx.x; i < W; i += 64) d[i] = s[i];
+}
+static_assert(sizeof(SimArgsPack) % 4 == 0, "SimArgsPack words");
+
 }  // namespace
 
 /* ====================================================================================== */
@@ -802,18 +1029,16 @@ int lds_bytes(int ring, int waves) {
  * persistent launch the long systems claimed last set the kernel's end at low occupancy.  The
  * budget pass therefore runs every system for at most 1 << log2 rounds and suspends the rest
  * (their state to HBM); the resume pass continues those (almost all long, of similar
- * remaining length) on a grid sized to an integral number of systems per slot.  Results are
+ * remaining length), sizing its own grid from the device-resident count.  Results are
  * identical: a system's rounds run in the same order, only split across two launches.
- * DSM_BUDGET_LOG2 (environment) overrides the budget; 0 turns the schedule off. */
-static uint32_t budget_log2() {
-    const char *e = getenv("DSM_BUDGET_LOG2");
-    if (e && *e) {
-        const long v = strtol(e, nullptr, 10);
-        return (v > 0 && v < (long)RSH_MAX) ? (uint32_t)v : 0u;
-    }
-    return 12;
+ * Defaults: budget 2^12, late budget 2^10; dsm_set_budget (or DSM_BUDGET_LOG2 /
+ * DSM_LATE_LOG2 in the environment at dsm_open) change them; budget 0 = one pass. */
+static uint32_t env_u32(const char *name, uint32_t dflt) {
+    const char *e = getenv(name);
+    if (!e || !*e) return dflt;
+    const long v = strtol(e, nullptr, 10);
+    return v < 0 ? 0u : (uint32_t)v;
 }
-
 
 #define ensure dsm_ensure
 
@@ -845,11 +1070,17 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->sched_thresh = DSM_SCHED_LOCKSTEP;
     c->ring = ring;
     c->cus = prop.multiProcessorCount;
+    /* tuning knobs: read here once, reported by dsm_launch_info_get */
+    c->budget_log2 = env_u32("DSM_BUDGET_LOG2", 12);
+    if (c->budget_log2 >= RSH_MAX) c->budget_log2 = 0;
+    c->late_log2 = env_u32("DSM_LATE_LOG2", 10);
+    c->round_limit_log2 = RSH_MAX;
+    c->inbox_limit = FB_RING;
+    c->fmt_tile = (int)env_u32("DSM_FMT", 132);
+    c->parse_bpl = (int)env_u32("DSM_PARSE_BPL", 32);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void **)&c->d_ctrl, CTRL_WORDS * sizeof(unsigned int)) != hipSuccess ||
-        hipMalloc((void **)&c->d_args, 3 * sizeof(SimArgs)) != hipSuccess ||
-        hipHostMalloc((void **)&c->h_args, 3 * sizeof(SimArgs), hipHostMallocDefault) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_args, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc((void **)&c->d_args, sizeof(SimArgsPack)) != hipSuccess ||
         hipMalloc((void **)&c->d_cnt, sizeof(dsm_counters)) != hipSuccess ||
         hipMalloc((void **)&c->d_table, DT_TABLE_WORDS * sizeof(uint32_t)) != hipSuccess) {
         dsm_close(c);
@@ -862,10 +1093,12 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
             return DSM_E_DEVICE;
         }
     }
-    if ((cfg->flags & DSM_F_TIMING) &&
-        (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)) {
-        dsm_close(c);
-        return DSM_E_DEVICE;
+    if (cfg->flags & DSM_F_TIMING) {
+        for (int i = 0; i < DSM_TIMING_RING; ++i)
+            if (hipEventCreate(&c->tev0[i]) != hipSuccess || hipEventCreate(&c->tev1[i]) != hipSuccess) {
+                dsm_close(c);
+                return DSM_E_DEVICE;
+            }
     }
     *out = c;
     return DSM_OK;
@@ -875,15 +1108,15 @@ extern "C" void dsm_close(dsm_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *ptrs[] = {c->d_ctrl, c->d_args, c->d_partials, c->d_ovf_list, c->d_susp, c->d_susp_list,
+    void *ptrs[] = {c->d_ctrl, c->d_args, c->d_ovf_list, c->d_susp, c->d_susp_list,
                     c->d_traces, c->d_counts,
                     c->d_res, c->d_cnt, c->d_recs, c->d_table, c->d_issue, c->d_issue_n};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     dsm_text_release(c);
-    if (c->h_args) (void)hipHostFree(c->h_args);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->ev_args) (void)hipEventDestroy(c->ev_args);
+    for (int i = 0; i < DSM_TIMING_RING; ++i) {
+        if (c->tev0[i]) (void)hipEventDestroy(c->tev0[i]);
+        if (c->tev1[i]) (void)hipEventDestroy(c->tev1[i]);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     free(c);
 }
@@ -894,7 +1127,28 @@ extern "C" int dsm_launch_info_get(dsm_ctx *c, dsm_launch_info *info) {
     return DSM_OK;
 }
 
-/* Run the transition kernel (+ 256-deep re-run of overflowing systems + counter reduce). */
+extern "C" int dsm_set_budget(dsm_ctx *c, uint32_t budget_log2, uint32_t late_log2) {
+    if (!c || budget_log2 >= RSH_MAX || late_log2 >= RSH_MAX) return DSM_E_INVAL;
+    c->budget_log2 = budget_log2;
+    c->late_log2 = late_log2;
+    return DSM_OK;
+}
+
+extern "C" int dsm_set_round_limit(dsm_ctx *c, uint32_t limit_log2) {
+    if (!c || limit_log2 > RSH_MAX) return DSM_E_INVAL;
+    c->round_limit_log2 = limit_log2 ? limit_log2 : RSH_MAX;
+    if (c->round_limit_log2 < 1) return DSM_E_INVAL;
+    return DSM_OK;
+}
+
+extern "C" int dsm_set_inbox_limit(dsm_ctx *c, uint32_t cap) {
+    if (!c || cap > (uint32_t)FB_RING) return DSM_E_INVAL;
+    c->inbox_limit = cap ? cap : (uint32_t)FB_RING;
+    return DSM_OK;
+}
+
+/* Run the transition kernel (+ resume pass, 256-deep re-run of overflowing systems, digest).
+ * Everything is enqueued on `st`; the host never waits. */
 static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys,
                       const uint16_t *d_traces, const uint32_t *d_counts, uint64_t n_sys,
                       dsm_sys_result *d_results, dsm_counters *d_counters, hipStream_t st) {
@@ -911,18 +1165,15 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fb, (const void *)fb, 64, 0));
     if (nb_fast < 1 || nb_fb < 1) return DSM_E_DEVICE;
     uint64_t want = (n_sys + (uint64_t)(FW * gpw) - 1) / (uint64_t)(FW * gpw);
-    int grid_fast = (int)((uint64_t)nb_fast * c->cus < want ? (uint64_t)nb_fast * c->cus : want);
+    const int grid_max = nb_fast * c->cus;
+    int grid_fast = (int)((uint64_t)grid_max < want ? (uint64_t)grid_max : want);
     int grid_fb = nb_fb * c->cus;
     if (grid_fb > 1024) grid_fb = 1024;
     uint64_t dblocks = (n_sys * np + 255) / 256;
     if (dblocks > (uint64_t)c->cus * 8) dblocks = (uint64_t)c->cus * 8;
-    /* two-pass schedule: the resume pass's partials follow the others (its grid is sized
-     * once the budget pass's suspended count is known) */
-    const uint32_t blog = (mode == 0 && !gen) ? budget_log2() : 0u;
-    const size_t waves = (size_t)grid_fast * FW + (size_t)grid_fb + (size_t)dblocks;
-    const size_t waves_cap = waves + (blog ? (size_t)grid_fast * FW : 0);
+    /* two-pass schedule on the packed path in bench mode */
+    const uint32_t blog = (mode == 0 && !gen) ? c->budget_log2 : 0u;
     int rc;
-    if ((rc = ensure(&c->d_partials, &c->partials_waves, waves_cap * K_N))) return rc;
     if ((rc = ensure(&c->d_ovf_list, &c->ovf_cap, (size_t)n_sys))) return rc;
     const int ring_eff = (mode && c->ring != 4) ? 12 : c->ring;   /* fast_mode's choice */
     if (blog) {
@@ -934,15 +1185,19 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
         if ((rc = ensure(&c->d_res, &c->res_cap, (size_t)n_sys + 1))) return rc;
         d_results = c->d_res;
     }
+    if (tr) {
+        const size_t cap = (size_t)np * c->cfg.max_instr;
+        if ((rc = ensure(&c->d_issue, &c->issue_cap_total, (size_t)n_sys * cap))) return rc;
+        if ((rc = ensure(&c->d_issue_n, &c->issue_n_cap, (size_t)n_sys))) return rc;
+    }
     if (c->cfg.flags & DSM_F_SNAPSHOTS)   /* nodes that never dump read back as zeros */
         HIPCK(hipMemsetAsync(c->d_recs, 0, (size_t)n_sys * np * 128, st));
     c->recs_n = n_sys;
     HIPCK(hipMemsetAsync(c->d_ctrl, 0, CTRL_WORDS * sizeof(unsigned int), st));
 
-    /* the pinned staging block may still be read by the previous run's copy */
-    HIPCK(hipEventSynchronize(c->ev_args));
-    SimArgs &A = c->h_args[0];
-    memset(&A, 0, sizeof A);
+    SimArgsPack pk;
+    memset(&pk, 0, sizeof pk);
+    SimArgs &A = pk.a[0];
     A.traces = d_traces;
     A.counts = d_counts;
     A.stride = c->cfg.max_instr;
@@ -953,94 +1208,74 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.dist = gen ? g->dist : 0;
     A.results = d_results;
     A.recs = c->d_recs;
-    A.partials = c->d_partials;
+    A.counters = reinterpret_cast<unsigned long long *>(d_counters);
     A.claim = c->d_ctrl + CTRL_FAST;
     A.ovf_list = c->d_ovf_list;
     A.ovf_count = c->d_ctrl + CTRL_OVF;
     A.table = c->d_table;
     A.sched_seed = c->sched_seed;
     A.sched_thresh = c->sched_thresh;
+    A.lim_rsh = c->round_limit_log2;
+    A.icap = c->inbox_limit;
     A.rsh = blog ? blog : RSH_MAX;
     A.budget = blog ? 1u : 0u;
-    {
-        const char *e = getenv("DSM_LATE_LOG2");
-        const long v = (e && *e) ? strtol(e, nullptr, 10) : 10;
-        A.late_rsh = (blog && v > 0 && (uint32_t)v < blog) ? (uint32_t)v : 0u;
-    }
+    A.late_rsh = (blog && c->late_log2 > 0 && c->late_log2 < blog) ? c->late_log2 : 0u;
     A.susp = c->d_susp;
     A.susp_list = c->d_susp_list;
     A.susp_count = c->d_ctrl + CTRL_SUSP;
     if (tr) {
-        const size_t cap = (size_t)np * c->cfg.max_instr;
-        if ((rc = ensure(&c->d_issue, &c->issue_cap_total, (size_t)n_sys * cap))) return rc;
-        if ((rc = ensure(&c->d_issue_n, &c->issue_n_cap, (size_t)n_sys))) return rc;
         A.issue = c->d_issue;
         A.issue_n = c->d_issue_n;
-        A.issue_cap = (uint32_t)cap;
+        A.issue_cap = (uint32_t)((size_t)np * c->cfg.max_instr);
         c->issue_sys = n_sys;
     }
-    SimArgs &B = c->h_args[1];
+    SimArgs &B = pk.a[1];           /* 256-deep re-run of the overflow list */
     B = A;
     B.d_n = c->d_ctrl + CTRL_OVF;
     B.list = c->d_ovf_list;
-    B.partials = c->d_partials + (size_t)grid_fast * FW * K_N;
     B.claim = c->d_ctrl + CTRL_FB;
     B.ovf_list = nullptr;
     B.ovf_count = nullptr;
     B.rsh = RSH_MAX;
     B.budget = 0;
-    HIPCK(hipMemcpyAsync(c->d_args, c->h_args, 2 * sizeof(SimArgs), hipMemcpyHostToDevice, st));
-    HIPCK(hipEventRecord(c->ev_args, st));
+    SimArgs &C = pk.a[2];           /* resume pass: the suspended list, count on the device */
+    C = A;
+    C.n_sys = 0;
+    C.d_n = c->d_ctrl + CTRL_SUSP;
+    C.list = c->d_susp_list;
+    C.claim = c->d_ctrl + CTRL_RES;
+    C.rsh = RSH_MAX;
+    C.budget = 0;
+    C.late_rsh = 0;
+    C.resume = 1;
+    hipLaunchKernelGGL(args_kernel, dim3(1), dim3(64), 0, st, pk, c->d_args);
+    HIPCK(hipGetLastError());
 
-    if (c->ev0) HIPCK(hipEventRecord(c->ev0, st));
+    const bool timed = (c->cfg.flags & DSM_F_TIMING) != 0;
+    const int slot = (int)(c->runs_timed % DSM_TIMING_RING);
+    if (timed) HIPCK(hipEventRecord(c->tev0[slot], st));
     hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, (const SimArgs *)c->d_args);
     HIPCK(hipGetLastError());
-    int grid_res = 0;
+    /* resume pass at the budget pass's grid: it sizes itself from the suspended count */
     if (blog) {
-        /* resume pass: every suspended system continues; the grid holds an integral number
-         * of them per slot, so the slots (all running systems of similar remaining length)
-         * finish together */
-        uint32_t n_res = 0;
-        HIPCK(hipMemcpyAsync(&n_res, c->d_ctrl + CTRL_SUSP, sizeof n_res, hipMemcpyDeviceToHost, st));
-        HIPCK(hipStreamSynchronize(st));
-        if (n_res) {
-            const uint64_t slots_max = (uint64_t)grid_fast * FW * gpw;
-            const uint64_t per = (n_res + slots_max - 1) / slots_max;
-            const uint64_t slots = (n_res + per - 1) / per;
-            grid_res = (int)((slots + (uint64_t)(FW * gpw) - 1) / (uint64_t)(FW * gpw));
-            SimArgs &C = c->h_args[2];
-            C = A;
-            C.n_sys = n_res;
-            C.d_n = c->d_ctrl + CTRL_SUSP;
-            C.list = c->d_susp_list;
-            C.partials = c->d_partials + waves * K_N;
-            C.claim = c->d_ctrl + CTRL_RES;
-            C.rsh = RSH_MAX;
-            C.budget = 0;
-            C.late_rsh = 0;
-            C.resume = 1;
-            HIPCK(hipMemcpyAsync(c->d_args + 2, &C, sizeof(SimArgs), hipMemcpyHostToDevice, st));
-            HIPCK(hipEventRecord(c->ev_args, st));
-            hipLaunchKernelGGL(fast, dim3(grid_res), dim3(64 * FW), 0, st, (const SimArgs *)(c->d_args + 2));
-            HIPCK(hipGetLastError());
-        }
+        hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, (const SimArgs *)(c->d_args + 2));
+        HIPCK(hipGetLastError());
     }
-    if (c->ev1) { HIPCK(hipEventRecord(c->ev1, st)); c->timed = 1; }
+    if (timed) {
+        HIPCK(hipEventRecord(c->tev1[slot], st));
+        c->runs_timed++;
+    }
 
     hipLaunchKernelGGL(fb, dim3(grid_fb), dim3(64), 0, st, (const SimArgs *)(c->d_args + 1));
     HIPCK(hipGetLastError());
 
-    unsigned long long *dpart = c->d_partials + ((size_t)grid_fast * FW + grid_fb) * K_N;
+    unsigned long long *dcnt = reinterpret_cast<unsigned long long *>(d_counters);
     if (np == 4)
         hipLaunchKernelGGL(digest_kernel<4>, dim3((unsigned)dblocks), dim3(256), 0, st, n_sys,
-                           (const uint4 *)c->d_recs, d_results, dpart);
+                           (const uint4 *)c->d_recs, d_results, dcnt);
     else
         hipLaunchKernelGGL(digest_kernel<8>, dim3((unsigned)dblocks), dim3(256), 0, st, n_sys,
-                           (const uint4 *)c->d_recs, d_results, dpart);
-    HIPCK(hipGetLastError());
-
-    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, st, c->d_partials,
-                       (int)(waves + (size_t)grid_res * FW), (unsigned long long *)d_counters);
+                           (const uint4 *)c->d_recs, d_results, dcnt);
     HIPCK(hipGetLastError());
 
     c->info.grid_blocks = grid_fast;
@@ -1048,11 +1283,16 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     c->info.waves_per_cu = nb_fast * FW;
     c->info.cus = c->cus;
     c->info.ring_cap = ring_eff;
-    c->info.resume_blocks = grid_res;
+    c->info.resume_blocks = blog ? grid_fast : 0;
     c->info.budget_log2 = (int)blog;
-    c->info.lds_bytes_per_block = lds_bytes(c->ring, FW);
+    c->info.lds_bytes_per_block = lds_bytes(ring_eff, FW);
+    c->info.late_log2 = (int)A.late_rsh;
+    c->info.round_limit_log2 = (int)c->round_limit_log2;
+    c->info.fmt_tile = c->fmt_tile;
+    c->info.parse_bpl = c->parse_bpl;
     return DSM_OK;
 }
+
 
 static int validate_host_traces(const dsm_ctx *c, const uint16_t *traces, const uint32_t *counts,
                                  uint64_t n_sys) {
@@ -1148,12 +1388,26 @@ extern "C" int dsm_generate_device(dsm_ctx *c, const dsm_gen *g, uint64_t first_
     return DSM_OK;
 }
 
+extern "C" int dsm_kernel_ms_history(dsm_ctx *c, float *ms, uint32_t cap, uint32_t *n) {
+    if (!c || !n || (cap && !ms)) return DSM_E_INVAL;
+    if (!(c->cfg.flags & DSM_F_TIMING)) return DSM_E_STATE;
+    HIPCK(hipSetDevice(c->device));
+    uint64_t k = c->runs_timed < DSM_TIMING_RING ? c->runs_timed : DSM_TIMING_RING;
+    if (k > cap) k = cap;
+    for (uint64_t i = 0; i < k; ++i) {       /* oldest first */
+        const int slot = (int)((c->runs_timed - k + i) % DSM_TIMING_RING);
+        HIPCK(hipEventSynchronize(c->tev1[slot]));
+        HIPCK(hipEventElapsedTime(&ms[i], c->tev0[slot], c->tev1[slot]));
+    }
+    *n = (uint32_t)k;
+    return DSM_OK;
+}
+
 extern "C" int dsm_last_kernel_ms(dsm_ctx *c, float *ms) {
     if (!c || !ms) return DSM_E_INVAL;
-    if (!c->ev0 || !c->timed) return DSM_E_STATE;
-    HIPCK(hipEventSynchronize(c->ev1));
-    HIPCK(hipEventElapsedTime(ms, c->ev0, c->ev1));
-    return DSM_OK;
+    if (!(c->cfg.flags & DSM_F_TIMING) || c->runs_timed == 0) return DSM_E_STATE;
+    uint32_t n = 0;
+    return dsm_kernel_ms_history(c, ms, 1, &n);
 }
 
 extern "C" int dsm_get_node_state(dsm_ctx *c, uint64_t sys, int node, dsm_node_state *dump,

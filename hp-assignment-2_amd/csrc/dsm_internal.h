@@ -12,6 +12,8 @@
 
 struct SimArgs;   /* transition-kernel argument block (dsm_engine.hip) */
 
+#define DSM_TIMING_RING 64
+
 struct dsm_ctx {
     int device;
     dsm_config cfg;
@@ -20,8 +22,6 @@ struct dsm_ctx {
     int cus;
     unsigned int *d_ctrl;            /* claim shards (fast, fallback) + overflow count      */
     SimArgs *d_args;                 /* [0] fast kernel, [1] 256-deep re-run, [2] resume    */
-    unsigned long long *d_partials;
-    size_t partials_waves;
     uint32_t *d_ovf_list;
     size_t ovf_cap;
     uint32_t *d_susp;                /* two-pass schedule: suspended node states             */
@@ -39,10 +39,16 @@ struct dsm_ctx {
     uint4 *d_recs;                   /* [sys][node][dump, final] node records of the last run */
     size_t recs_cap;
     uint64_t recs_n;
-    SimArgs *h_args;                 /* pinned host staging for the argument blocks         */
-    hipEvent_t ev0, ev1, ev_args;
-    int timed;
+    /* DSM_F_TIMING: event pairs around the transition launches of the last DSM_TIMING_RING
+     * runs (run k uses slot k % DSM_TIMING_RING) */
+    hipEvent_t tev0[DSM_TIMING_RING], tev1[DSM_TIMING_RING];
+    uint64_t runs_timed;
     dsm_launch_info info;
+    /* two-pass schedule and round limit (dsm_set_budget / dsm_set_round_limit; defaults from
+     * DSM_BUDGET_LOG2 / DSM_LATE_LOG2, read once at dsm_open) */
+    uint32_t budget_log2, late_log2, round_limit_log2, inbox_limit;
+    /* dsm_text.hip tuning (DSM_FMT / DSM_PARSE_BPL, read once at dsm_open) */
+    int fmt_tile, parse_bpl;
     uint64_t sched_seed;             /* dsm_set_schedule                                     */
     uint32_t sched_thresh;
     uint32_t *d_issue;               /* DSM_F_ISSUE_TRACE: [sys][np * max_instr] events      */

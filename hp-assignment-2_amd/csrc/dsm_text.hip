@@ -516,9 +516,8 @@ static int ensure_templates(dsm_ctx *c) {
  * from L2) or 100 + FR (108, 116, 132: templates resident in LDS, next tile's records
  * prefetched) for A/B runs.  Measured on 8M records (tools/ab_fmt.py): 16 5.47 ms, 116 3.40,
  * 132 3.35 (5.1 TB/s) -- the default. */
-static int fmt_choice() {
-    const char *e = getenv("DSM_FMT");
-    const int v = e ? atoi(e) : 132;
+static int fmt_choice(const dsm_ctx *c) {      /* c->fmt_tile: DSM_FMT, read at dsm_open */
+    const int v = c->fmt_tile;
     return (v == 4 || v == 8 || v == 16 || v == 108 || v == 116) ? v : 132;   /* 1xx: LDS templates */
 }
 
@@ -527,7 +526,7 @@ static int launch_fmt(dsm_ctx *c, const uint8_t *recs, uint64_t stride_bytes, ui
     if (n == 0) return DSM_OK;
     int rc = ensure_templates(c);
     if (rc) return rc;
-    const int v = fmt_choice(), fr = v % 100;
+    const int v = fmt_choice(c), fr = v % 100;
     const bool tl = v >= 100;
     const void *fn = tl ? (fr == 8 ? (const void *)fmt_kernel<8, 128, true>
                            : fr == 32 ? (const void *)fmt_kernel<32, 512, true> : (const void *)fmt_kernel<16, 256, true>)
@@ -612,9 +611,9 @@ extern "C" int dsm_parse_traces_device(dsm_ctx *c, const char *d_text, const uin
     if (n_files && (!d_text || !d_offsets || !d_traces || !d_counts)) return DSM_E_INVAL;
     if (n_files == 0) return DSM_OK;
     HIPCK(hipSetDevice(c->device));
-    /* DSM_PARSE_BPL=16|32: bytes per lane per window (1 or 2 KB windows), for A/B runs */
-    const char *e = getenv("DSM_PARSE_BPL");
-    const bool b32 = e ? atoi(e) == 32 : true;
+    /* DSM_PARSE_BPL=16|32 (read at dsm_open): bytes per lane per window (1 or 2 KB
+     * windows), for A/B runs */
+    const bool b32 = c->parse_bpl != 16;
     const void *fn = b32 ? (const void *)parse_kernel<32> : (const void *)parse_kernel<16>;
     /* one resident round of workgroups: a grid-stride loop over files with a second, partial
      * round of workgroups would leave most of the chip idle at the end */

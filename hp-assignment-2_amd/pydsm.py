@@ -31,7 +31,8 @@ COUNTER_FIELDS = ([f"msgs_{t}" for t in TYPE_NAMES] +
                   ["msgs", "instrs", "rounds", "systems"] +
                   [f"status_{s}" for s in STATUS_NAMES] +
                   ["sum_dump_hash", "sum_final_hash", "max_rounds", "overflow_reruns",
-                   "wave_rounds", "resumed"] + [f"reserved{i}" for i in range(4)])
+                   "wave_rounds", "resumed", "ff_passes", "ff_steps"] +
+                  [f"reserved{i}" for i in range(2)])
 assert len(COUNTER_FIELDS) == 32
 
 DUMP_BASE, DUMP_MAX, DUMP_SLOT = 1954, 1958, 1968
@@ -58,7 +59,9 @@ class LaunchInfo(ctypes.Structure):
     _fields_ = [("grid_blocks", ctypes.c_int), ("block_threads", ctypes.c_int),
                 ("waves_per_cu", ctypes.c_int), ("cus", ctypes.c_int),
                 ("ring_cap", ctypes.c_int), ("lds_bytes_per_block", ctypes.c_int),
-                ("resume_blocks", ctypes.c_int), ("budget_log2", ctypes.c_int)]
+                ("resume_blocks", ctypes.c_int), ("budget_log2", ctypes.c_int),
+                ("late_log2", ctypes.c_int), ("round_limit_log2", ctypes.c_int),
+                ("fmt_tile", ctypes.c_int), ("parse_bpl", ctypes.c_int)]
 
 
 _lib = None
@@ -93,6 +96,10 @@ def lib():
             "dsm_run_generated": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp]),
             "dsm_get_node_state": (i32, [vp, u64, i32, vp, vp]),
             "dsm_last_kernel_ms": (i32, [vp, ctypes.POINTER(ctypes.c_float)]),
+            "dsm_kernel_ms_history": (i32, [vp, vp, u32, ctypes.POINTER(u32)]),
+            "dsm_set_budget": (i32, [vp, u32, u32]),
+            "dsm_set_round_limit": (i32, [vp, u32]),
+            "dsm_set_inbox_limit": (i32, [vp, u32]),
             "dsm_parse_trace_file": (i32, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
             "dsm_load_test_dir": (i32, [ctypes.c_char_p, i32, u32, vp, u32, vp]),
             "dsm_format_dump": (i32, [i32, vp, ctypes.c_char_p, ctypes.c_size_t]),
@@ -286,6 +293,23 @@ class Engine:
         ms = ctypes.c_float(0)
         _check(lib().dsm_last_kernel_ms(self.ctx, ctypes.byref(ms)), "dsm_last_kernel_ms")
         return float(ms.value)
+
+    def kernel_ms_history(self, cap=64):
+        """Transition-kernel device times (ms) of the last min(cap, 64) runs, oldest first."""
+        ms = np.zeros(max(cap, 1), dtype=np.float32)
+        n = ctypes.c_uint32(0)
+        _check(lib().dsm_kernel_ms_history(self.ctx, _ptr(ms), cap, ctypes.byref(n)),
+               "dsm_kernel_ms_history")
+        return [float(x) for x in ms[:n.value]]
+
+    def set_budget(self, budget_log2, late_log2=10):
+        _check(lib().dsm_set_budget(self.ctx, budget_log2, late_log2), "dsm_set_budget")
+
+    def set_round_limit(self, limit_log2):
+        _check(lib().dsm_set_round_limit(self.ctx, limit_log2), "dsm_set_round_limit")
+
+    def set_inbox_limit(self, cap):
+        _check(lib().dsm_set_inbox_limit(self.ctx, cap), "dsm_set_inbox_limit")
 
     def launch_info(self):
         li = LaunchInfo()

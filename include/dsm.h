@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DSM_ABI_VERSION 1
+#define DSM_ABI_VERSION 2
 
 #define DSM_MAX_NP 8             /* bitVector is one byte (README.md:51)                  */
 #define DSM_CACHE_SIZE 4         /* CACHE_SIZE      assignment.c:10                        */
@@ -148,7 +148,9 @@ typedef struct dsm_counters {
     uint64_t overflow_reruns;  /* systems re-run with the 256-deep inbox */
     uint64_t wave_rounds;      /* lock-step loop iterations summed over waves (cost model) */
     uint64_t resumed;          /* systems the two-pass schedule suspended and resumed      */
-    uint64_t reserved[4];
+    uint64_t ff_passes;        /* hit-run fast-forward passes (per wave, cost model)        */
+    uint64_t ff_steps;         /* their 8-instruction steps (per wave, cost model)          */
+    uint64_t reserved[2];
 } dsm_counters;
 
 typedef struct dsm_ctx dsm_ctx;
@@ -163,6 +165,10 @@ typedef struct dsm_launch_info {
     int lds_bytes_per_block;
     int resume_blocks;     /* two-pass schedule: workgroups of the resume pass (0: none)   */
     int budget_log2;       /* its budget pass's round budget, log2 (0: one pass)          */
+    int late_log2;         /* the budget once a wave finds no new system, log2 (0: none)   */
+    int round_limit_log2;  /* ROUND_LIMIT after 1 << this many active rounds               */
+    int fmt_tile;          /* dump formatter tile (DSM_FMT at dsm_open)                   */
+    int parse_bpl;         /* trace parser bytes per lane per window (DSM_PARSE_BPL)       */
 } dsm_launch_info;
 
 /* ---- library ---------------------------------------------------------------------- */
@@ -183,7 +189,11 @@ int dsm_run_packed(dsm_ctx *ctx, const uint16_t *traces, const uint32_t *counts,
 
 /* Device buffers (e.g. torch-owned HBM), asynchronous on `stream` (hipStream_t; NULL =
  * null stream).  d_results may be NULL; d_counters (device, one dsm_counters) is
- * ACCUMULATED into.  No host synchronisation inside. */
+ * ACCUMULATED into.  No host synchronisation inside: every launch (including the two-pass
+ * schedule's resume pass, which sizes itself on the device) is enqueued on `stream`.
+ * Device traces are not validated: a count above max_instr is clamped to max_instr, and an
+ * instruction whose home node (address >> 4) is >= np ends its system with
+ * DSM_ASSERT_FAILED (the reference would index out of bounds, assignment.c:90). */
 int dsm_run_packed_device(dsm_ctx *ctx, const uint16_t *d_traces, const uint32_t *d_counts,
                           uint64_t n_sys, dsm_sys_result *d_results,
                           dsm_counters *d_counters, void *stream);
@@ -226,9 +236,23 @@ int dsm_get_issue_trace(dsm_ctx *ctx, uint64_t sys, uint32_t *events, uint32_t c
 int dsm_format_issue_trace(const uint32_t *events, uint32_t n, char *buf, size_t cap);
 
 /* Device time of the transition kernel of the last run (needs DSM_F_TIMING): HIP events
- * recorded on the run's own stream right before and after the kernel launch.  Waits for
- * the stop event. */
+ * recorded on the run's own stream right before and after its launches (budget + resume
+ * pass).  Waits for the stop event. */
 int dsm_last_kernel_ms(dsm_ctx *ctx, float *ms);
+/* The same for the last min(cap, runs, 64) runs, oldest first; *n = how many. */
+int dsm_kernel_ms_history(dsm_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);
+
+/* Two-pass schedule of the packed path (bench mode): the budget pass suspends systems still
+ * running after 1 << budget_log2 rounds (0 = one pass), 1 << late_log2 once a wave finds no
+ * new system (0 = off); the resume pass continues them.  Results never depend on it.
+ * Defaults 12 / 10 (or DSM_BUDGET_LOG2 / DSM_LATE_LOG2 at dsm_open). */
+int dsm_set_budget(dsm_ctx *ctx, uint32_t budget_log2, uint32_t late_log2);
+/* Round limit of the following runs: a system still active after 1 << limit_log2 rounds
+ * stops with DSM_ROUND_LIMIT (1 <= limit_log2 <= 22; 0 = DSM_MAX_ROUNDS). */
+int dsm_set_round_limit(dsm_ctx *ctx, uint32_t limit_log2);
+/* Inbox limit of the following runs (MSG_BUFFER_SIZE, assignment.c:12; 1..256, 0 = 256): an
+ * append beyond it ends the system with DSM_RING_OVERFLOW (the reference spins, :715-724). */
+int dsm_set_inbox_limit(dsm_ctx *ctx, uint32_t cap);
 
 /* ---- initializeProcessor's trace reader on the GPU (:802-818) ---------------------- *
  * n_files core files concatenated in d_text; file f is d_text[d_offsets[f] .. d_offsets[f+1])

@@ -78,7 +78,15 @@ static void evict_line(osys *y, int me, int idx) {
     stage(y, a >> 4, m);
 }
 
-#define OASSERT(c) do { if (!(c)) { y->assert_failed = 1; return; } } while (0)
+/* branch probes for tools/find_scenarios.c (scenario search); compiled out otherwise */
+#ifdef ORC_PROBE
+void orc_probe(int id);
+#define PROBE(id) orc_probe(id)
+#else
+#define PROBE(id) ((void)0)
+#endif
+
+#define OASSERT(c) do { if (!(c)) { PROBE(1000 + __LINE__); y->assert_failed = 1; return; } } while (0)
 
 /* message switch :177-566 */
 static void handle(osys *y, int me, omsg m) {
@@ -100,7 +108,8 @@ static void handle(osys *y, int me, omsg m) {
         } else {                                                     /* :210-234 */
             int o = find_owner(y, s->dir_bv[blk]);
             OASSERT(o != -1);
-            if (o == m.sender) {
+            if (o == m.sender) {                                     /* :215-221 */
+                PROBE(1);
                 r.value = s->memory[blk]; r.bv = 2; stage(y, m.sender, r);
             } else {
                 omsg f = mk(WRITEBACK_INT, me, m.addr); f.r2 = m.sender;
@@ -156,6 +165,7 @@ static void handle(osys *y, int me, omsg m) {
         } else if (s->cache_addr[idx] == m.addr && s->cache_state[idx] == M_) {
             /* no change :337-338 */
         } else {
+            PROBE(3);
             SET_WAITING(nd, 0);                                      /* :345-346 */
             break;
         }
@@ -182,7 +192,8 @@ static void handle(osys *y, int me, omsg m) {
         } else {                                                     /* :405-433 */
             int o = find_owner(y, s->dir_bv[blk]);
             OASSERT(o != -1);
-            if (o == m.sender) {
+            if (o == m.sender) {                                     /* :410-418 */
+                PROBE(2);
                 stage(y, m.sender, mk(REPLY_WR, me, m.addr));
             } else {
                 omsg f = mk(WRITEBACK_INV, me, m.addr); f.r2 = m.sender;
@@ -205,6 +216,8 @@ static void handle(osys *y, int me, omsg m) {
             stage(y, H, r);
             if (m.r2 != H) stage(y, m.r2, r);
             s->cache_state[idx] = I_;
+        } else {
+            PROBE(4);                             /* ignored (deadlock source) :467-472 */
         }
         break;
     case FLUSH_INVACK:                                               /* :475-496 */
@@ -236,6 +249,8 @@ static void handle(osys *y, int me, omsg m) {
         } else if (m.sender == H) {                                  /* :526-532 */
             if (s->cache_addr[idx] == m.addr && s->cache_state[idx] == S_)
                 s->cache_state[idx] = E_;
+        } else {
+            PROBE(5);                             /* not from the home: ignored :533-537 */
         }
         break;
     case EVICT_MODIFIED:                                             /* :541-561 */
@@ -269,6 +284,7 @@ static void issue(osys *y, int me, uint16_t ins) {
         s->pending = v;                                              /* :633 */
         if (hit) {
             if (s->cache_state[idx] == M_ || s->cache_state[idx] == E_) {   /* :640-645 */
+                if (s->cache_state[idx] == E_) PROBE(6);
                 s->cache_value[idx] = v; s->cache_state[idx] = M_;
             } else {                                                 /* SHARED :646-659 */
                 stage(y, H, mk(UPGRADE, me, a));
@@ -312,6 +328,11 @@ typedef struct {
     uint64_t seed; uint32_t thresh; uint64_t sys;      /* schedule (dsm_sched_act)         */
     uint32_t *ev; uint32_t ev_cap; uint32_t ev_n;       /* issue order: node << 16 | instr   */
 } oextra;
+
+/* round limit of the following runs (orc_set_round_limit; the reference loops forever, the
+ * build reports ST_ROUND_LIMIT after this many active rounds) */
+static uint32_t g_round_limit = DSM_ROUND_LIMIT;
+void orc_set_round_limit(uint32_t limit) { g_round_limit = limit ? limit : DSM_ROUND_LIMIT; }
 
 static int run_one(int np, const tsrc *t, const uint32_t *counts, uint32_t ring_cap,
                    dsm_res *res, dsm_rec *dump_out, dsm_rec *fin_out, uint64_t *by_type,
@@ -380,7 +401,7 @@ static int run_one(int np, const tsrc *t, const uint32_t *counts, uint32_t ring_
             break;
         }
         rounds = r;
-        if (r >= DSM_ROUND_LIMIT) { status = ST_ROUND_LIMIT; break; }
+        if (r >= g_round_limit) { status = ST_ROUND_LIMIT; break; }
     }
     uint32_t mask = 0;
     uint64_t dh = 0, fh = 0;

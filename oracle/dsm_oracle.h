@@ -42,6 +42,10 @@ int orc_run_packed_ex(int np, const uint16_t *traces, const uint32_t *counts, ui
                       dsm_rec *fin, uint32_t *issue, uint32_t issue_cap, uint32_t *issue_n,
                       int nthreads);
 
+/* Round limit (active rounds before ST_ROUND_LIMIT) of the following runs; 0 = the default
+ * DSM_ROUND_LIMIT.  Process-wide (test use). */
+void orc_set_round_limit(uint32_t limit);
+
 /* Fill traces [sys][node][n_instr] and counts [sys][node] from the generator. */
 void orc_generate(int np, int dist, uint64_t seed, uint32_t n_instr, uint64_t first_sys,
                   uint64_t n_sys, uint16_t *traces, uint32_t *counts);

@@ -36,6 +36,8 @@ def lib():
         L.orc_format_dump.argtypes = [i32, vp, ctypes.c_char_p, i32]
         L.orc_hash_rec.argtypes = [i32, vp, i32]
         L.orc_hash_rec.restype = u64
+        L.orc_set_round_limit.argtypes = [u32]
+        L.orc_set_round_limit.restype = None
         _lib = L
     return _lib
 
@@ -99,6 +101,11 @@ def run_generated(np_, dist, seed, n_instr, first, n, ring_cap=256, nthreads=8):
                                  _p(res), _p(bt), nthreads)
     assert rc == 0
     return res, bt
+
+
+def set_round_limit(limit):
+    """Active rounds before ST_ROUND_LIMIT for the following runs (0 = default 2^22)."""
+    lib().orc_set_round_limit(limit)
 
 
 def generate(np_, dist, seed, n_instr, first, n):

@@ -148,6 +148,10 @@ static void reset_ctx(int t) {
 /* seeded schedule exploration (dsm_common.h dsm_sched_act); lock-step by default */
 static uint64_t g_sched_seed, g_sys;
 static uint32_t g_sched_thresh = DSM_SCHED_LOCKSTEP;
+/* round limit: DSM_ROUND_LIMIT, or DSM_REF_ROUND_LIMIT from the environment (tests) */
+static uint32_t g_round_limit = DSM_ROUND_LIMIT;
+/* inbox limit: MSG_BUFFER_SIZE (:12), or DSM_REF_INBOX_LIMIT (tests; <= MSG_BUFFER_SIZE) */
+static int g_inbox_limit = MSG_BUFFER_SIZE;
 
 static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
     uint32_t rounds = 0, msgs = 0, instrs = 0, status = ST_COMPLETED;
@@ -183,7 +187,7 @@ static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
         int ovf = (nst > MAX_STAGED);
         for (int k = 0; k < nst && !ovf; ++k) {
             nodeCtx *d = &C[st_dest[k]];
-            if (d->count >= MSG_BUFFER_SIZE) { ovf = 1; break; }
+            if (d->count >= g_inbox_limit) { ovf = 1; break; }
             d->ring[(d->head + d->count) % MSG_BUFFER_SIZE] = st_msg[k];
             d->count++;
         }
@@ -195,7 +199,7 @@ static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
             break;
         }
         rounds = r;
-        if (r >= DSM_ROUND_LIMIT) { status = ST_ROUND_LIMIT; break; }
+        if (r >= g_round_limit) { status = ST_ROUND_LIMIT; break; }
     }
     uint32_t mask = 0;
     uint64_t dh = 0, fh = 0;
@@ -225,6 +229,12 @@ static void write_sys(FILE *f, const dsm_res *res, const dsm_rec *dump, const ds
 int main(int argc, char **argv) {
     dsm_res res;
     dsm_rec dump[NUM_PROCS], fin[NUM_PROCS];
+    {
+        const char *e = getenv("DSM_REF_ROUND_LIMIT");
+        if (e && *e && strtoul(e, 0, 0) > 0) g_round_limit = (uint32_t)strtoul(e, 0, 0);
+        e = getenv("DSM_REF_INBOX_LIMIT");
+        if (e && *e && atoi(e) > 0 && atoi(e) <= MSG_BUFFER_SIZE) g_inbox_limit = atoi(e);
+    }
     if (argc == 8 && !strcmp(argv[1], "tests")) {
         /* n schedule-exploration variants (system ids first .. first+n-1) of one test */
         g_sched_seed = strtoull(argv[4], 0, 0);

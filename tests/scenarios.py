@@ -175,3 +175,94 @@ def eight_nodes_all_read_one_block():
         assert dirent(fin[3], 5)[0] in (EM, DS)
         assert int(res["msgs"]) >= 8
     return tr, cn, check
+
+
+# ---- rows found by tools/find_scenarios.c (oracle branch probes, shrunk), derived by hand --
+
+@scenario
+def read_request_em_owner_is_requester():
+    """READ_REQUEST at a home whose EM owner IS the requester (:215-221): REPLY_RD exclusive,
+    no WRITEBACK_INT, no directory change.  Home 2 serves 0x21.  R2: node 1 reads (U ->
+    EM{1}).  R5: node 0's WRITE_REQUEST(20): EM owner 1 -> WRITEBACK_INV(r2=0), bv {0}.  R6:
+    node 1 flushes FLUSH_INVACK(41); home 2's own READ_REQUEST meets EM{0} -> WRITEBACK_INT(r2=2)
+    to node 0, S{0,2}.  R7: node 0 installs the flushed 41 as M (its 20 is lost); node 3's
+    WRITE_REQUEST(121) meets S{0,2} -> REPLY_ID{0,2}, EM{3}.  R8: the home part of node 1's
+    FLUSH_INVACK arrives late and sets EM{r2 = 0} over EM{3} (:478-480); node 0 flushes to the
+    home (S); node 3 installs 121 as M and invalidates 0 and 2.  R10: node 0 reads 0x21 again:
+    the home is EM{0} with owner == requester, so it answers REPLY_RD(41, exclusive) at R11.
+    Node 0 ends EXCLUSIVE while node 3 holds the line MODIFIED."""
+    tr, cn = build(4, [[("WR", 0x15, 128), ("WR", 0x21, 20), ("RD", 0x21)], [("RD", 0x21)],
+                       [("RD", 0x01), ("RD", 0x21)], [("WR", 0x35, 248), ("WR", 0x21, 121)]])
+
+    def check(res, dump, fin):
+        assert int(res["status"]) == COMPLETED | (0xF << 8)
+        assert (int(res["rounds"]), int(res["msgs"]), int(res["instrs"])) == (13, 24, 8)
+        assert dirent(fin[2], 1) == (EM, 0x01)
+        assert mem(fin[2], 1) == 41
+        assert line(fin[0], 1) == (0x21, 41, E)
+        assert line(fin[3], 1) == (0x21, 121, M)
+        assert int(fin[0][60]) == 20               # node 0's pending write, lost
+    return tr, cn, check
+
+
+@scenario
+def write_request_em_owner_is_requester():
+    """WRITE_REQUEST at a home whose EM owner IS the requester (:410-418): memory takes the
+    value first (:379), REPLY_WR, no WRITEBACK_INV, bv unchanged.  Home 1 serves 0x11.  R10:
+    the home part of a FLUSH_INVACK with r2 = 3 sets EM{3}.  R12: node 3 write-misses 0x11
+    (its line was invalidated) -> WRITE_REQUEST(89); R13: EM owner 3 == requester: memory =
+    89, REPLY_WR; R14: node 3 installs 89 as M.  Node 0 also holds 0x11 MODIFIED (155, from a
+    REPLY_ID at R10)."""
+    tr, cn = build(4, [[("WR", 0x15, 192), ("RD", 0x35), ("WR", 0x11, 155)], [("WR", 0x11, 120)],
+                       [("RD", 0x31), ("RD", 0x11)], [("WR", 0x11, 51), ("WR", 0x11, 89)]])
+
+    def check(res, dump, fin):
+        assert int(res["status"]) == COMPLETED | (0xF << 8)
+        assert (int(res["rounds"]), int(res["msgs"]), int(res["instrs"])) == (15, 25, 8)
+        assert mem(fin[1], 1) == 89
+        assert dirent(fin[1], 1) == (EM, 0x08)
+        assert line(fin[3], 1) == (0x11, 89, M)
+        assert line(fin[0], 1) == (0x11, 155, M)
+    return tr, cn, check
+
+
+@scenario
+def ignored_writeback_inv_deadlocks_requester():
+    """WRITEBACK_INV at a node whose line no longer holds the block (:467-472): ignored, no
+    FLUSH_INVACK, so the requester waits forever.  R8: node 0 write-misses 0x19 (its line was
+    flushed-invalidated at R7) -> WRITE_REQUEST(6).  R9: home 1 writes 6, EM owner 3 ->
+    WRITEBACK_INV(r2=0) to node 3, bv {0}; the same round node 3 evicts 0x19 (M, 29) to take
+    0x01.  R10: node 3's line holds 0x01: the WRITEBACK_INV is ignored; home 1 stores the
+    evicted 29 over the 6 (EVICT_MODIFIED, :543) and keeps EM{0} (sender 3 not in bv).
+    Node 0 deadlocks; nodes 1-3 dump."""
+    tr, cn = build(4, [[("WR", 0x25, 199), ("RD", 0x19), ("WR", 0x19, 6)], [], [],
+                       [("RD", 0x01), ("WR", 0x19, 48), ("WR", 0x01, 2)]])
+
+    def check(res, dump, fin):
+        assert int(res["status"]) == DEADLOCKED | (0b1110 << 8)
+        assert (int(res["rounds"]), int(res["msgs"]), int(res["instrs"])) == (12, 17, 6)
+        assert int(fin[0][61]) & 1 == 1           # node 0 still waitingForReply
+        assert line(fin[0], 1) == (0x19, 0, I)
+        assert mem(fin[1], 9) == 29
+        assert dirent(fin[1], 9) == (EM, 0x01)
+        assert line(fin[3], 1) == (0x01, 2, M)
+        assert mem(fin[0], 1) == 2 and dirent(fin[0], 1) == (EM, 0x08)
+    return tr, cn, check
+
+
+@scenario
+def write_hit_on_exclusive_is_local():
+    """Write hit on an EXCLUSIVE line (:640-645): value and state M locally, no message.
+    Node 1 reads its own block 0x19 (R1 READ_REQUEST to itself, R2 U -> EM{1}, R3 installs
+    29 EXCLUSIVE), then writes 120 at R4: MODIFIED 120, memory keeps 29; R5 dump."""
+    tr, cn = build(4, [[], [("RD", 0x19), ("WR", 0x19, 120)], [], []])
+
+    def check(res, dump, fin):
+        assert int(res["status"]) == COMPLETED | (0xF << 8)
+        assert (int(res["rounds"]), int(res["msgs"]), int(res["instrs"])) == (5, 2, 2)
+        assert line(fin[1], 1) == (0x19, 120, M)
+        assert line(dump[1], 1) == (0x19, 120, M)
+        assert int(fin[1][60]) == 120
+        assert mem(fin[1], 9) == 29
+        assert dirent(fin[1], 9) == (EM, 0x02)
+    return tr, cn, check

@@ -1,0 +1,38 @@
+"""GPU: bench.py end to end on the one GPU of the box -- the 1-rank line, and `--gpus 2`
+through its own launcher (both ranks on device 0, counters over gloo: RCCL needs a GPU per
+rank), whose whole-job counters must equal one rank simulating both shards."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+SMALL = ["--systems", "32768", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-dump",
+         "--parse-systems", "0"]
+
+
+def _bench(args, env=None, timeout=240):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, cwd=REPO,
+                       capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_two_rank_launch_equals_one_rank_over_both_shards():
+    two = _bench(["--gpus", "2"] + SMALL,
+                 env={"DSM_BENCH_BACKEND": "gloo", "DSM_BENCH_DEVICE": "0"})
+    one = _bench(["--gpus", "1"] + SMALL[:1] + ["65536"] + SMALL[2:])
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["parallelism"] == "ensemble-dp2"
+    for k in ("msgs", "instrs", "rounds", "systems", "max_rounds", "status_DEADLOCKED"):
+        assert two["counters"][k] == one["counters"][k], k
+    assert two["sum_final_hash"] == one["sum_final_hash"]
+    assert two["value"] > 0 and two["roofline"]["achieved"] > 0

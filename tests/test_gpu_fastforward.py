@@ -1,0 +1,127 @@
+"""GPU: the hit-run fast-forward of the transition kernel (dsm_engine.hip step (4b)).
+
+After a round in which a system sent nothing, every further round until some node issues a
+sending instruction is one local hit per non-waiting node (assignment.c:607-611 RD hit,
+:635-645 WR hit on M/E); the kernel applies such runs 8 rounds per step.  It must be exact:
+results (rounds included), records and counters equal the oracle's, and equal the kernel's
+own round-by-round path (the issue-order mode, which has no fast-forward)."""
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import ORACLE, golden_ensemble, res_to_u64
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dsm():
+    import pydsm
+    if pydsm.device_count() < 1:
+        pytest.fail("gpu tests need a GPU (no fallback exists)")
+    return pydsm
+
+
+@pytest.fixture(scope="module")
+def orc():
+    import pyoracle
+    return pyoracle
+
+
+def _cmp(a, b):
+    a, b = res_to_u64(a), (b if b.ndim == 2 else res_to_u64(b))
+    bad = np.nonzero((a != b).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} of {len(a)} systems differ; first {bad[:4]}: {a[bad[:2]]} vs {b[bad[:2]]}"
+
+
+@pytest.mark.parametrize("np_,dist,ring", [(8, "hot", 12), (8, "hot", 4), (4, "hot", 12),
+                                            (8, "uniform", 12), (8, "evict", 8)])
+def test_packed_fast_forward_vs_oracle(dsm, orc, np_, dist, ring):
+    """Packed traces (budget + resume passes, fast-forward in both), records included."""
+    n = 4096
+    tr, cn = orc.generate(np_, dist, 17, 4096, 123, n)
+    with dsm.Engine(np_, 4096, ring_cap=ring, snapshots=True) as eng:
+        res, cnt = eng.run_packed(tr, cn)
+        ores, _, odump, ofin = orc.run_packed(np_, tr, cn, records=True, nthreads=16)
+        for s in range(0, n, 61):
+            mask = int(ores[s]["status"]) >> 8
+            for nd in range(np_):
+                d, f = eng.node_state(s, nd)
+                assert np.array_equal(f, ofin[s, nd])
+                if (mask >> nd) & 1:
+                    assert np.array_equal(d, odump[s, nd])
+    _cmp(res, ores)
+    assert cnt["msgs"] == int(ores["msgs"].sum()) and cnt["instrs"] == int(ores["instrs"].sum())
+    if dist == "hot":
+        assert cnt["ff_passes"] > 0 and cnt["ff_steps"] > cnt["ff_passes"]
+
+
+def test_fast_forward_equals_round_by_round(dsm, orc):
+    """The issue-order mode runs every round (no fast-forward): same results, fewer rounds
+    of the wave loop with it."""
+    n = 2048
+    tr, cn = orc.generate(8, "hot", 5, 4096, 0, n)
+    with dsm.Engine(8, 4096) as eng:
+        a, ca = eng.run_packed(tr, cn)
+    with dsm.Engine(8, 4096, issue_trace=True) as eng:
+        b, cb = eng.run_packed(tr, cn)
+    assert np.array_equal(res_to_u64(a), res_to_u64(b))
+    assert cb["ff_passes"] == 0 and ca["ff_passes"] > 0
+    assert ca["wave_rounds"] * 2 < cb["wave_rounds"]
+
+
+def test_generated_hot_golden(dsm, ensemble_meta):
+    """The fused-generator path (fast-forward over generated chunks) against the golden
+    fixture pinned by the reference's handler text."""
+    m = ensemble_meta["np8_hot"]
+    with dsm.Engine(8, 4096) as eng:
+        res, cnt = eng.run_generated(m["dist"], m["seed"], m["n_instr"], m["first_sys"], m["n_sys"])
+    _cmp(res, golden_ensemble("np8_hot"))
+    assert cnt["ff_passes"] > 0
+
+
+@pytest.mark.parametrize("limit_log2", [6, 10])
+def test_round_limit_inside_hit_runs(dsm, orc, limit_log2):
+    """ROUND_LIMIT at 2^k rounds: the fast-forward stops exactly at the limit (hot systems
+    are mostly inside hit runs there); packed and generated paths, against the oracle."""
+    n = 2048
+    tr, cn = orc.generate(8, "hot", 9, 4096, 500, n)
+    orc.set_round_limit(1 << limit_log2)
+    try:
+        ores, _, _, ofin = orc.run_packed(8, tr, cn, records=True, nthreads=16)
+        gres, _ = orc.run_generated(8, "hot", 9, 4096, 500, n, nthreads=16)
+    finally:
+        orc.set_round_limit(0)
+    assert int(((ores["status"] & 0xFF) == 4).sum()) > n // 2
+    with dsm.Engine(8, 4096, snapshots=True) as eng:
+        eng.set_round_limit(limit_log2)
+        res, cnt = eng.run_packed(tr, cn)
+        for s in range(0, n, 97):
+            assert np.array_equal(eng.node_state(s, 3)[1], ofin[s, 3])
+        g, _ = eng.run_generated("hot", 9, 4096, 500, n)
+        assert eng.launch_info()["round_limit_log2"] == limit_log2
+    _cmp(res, ores)
+    _cmp(g, gres)
+    assert cnt["status_ROUND_LIMIT"] == int(((ores["status"] & 0xFF) == 4).sum())
+    assert cnt["max_rounds"] == 1 << limit_log2
+
+
+def test_round_limit_matches_reference_text(dsm, orc):
+    """The same limit on the reference's own handler text (oracle/_ref, where built)."""
+    b = os.path.join(ORACLE, "_ref", "ref_lockstep_np8")
+    if not os.path.exists(b):
+        pytest.skip("oracle/_ref not built")
+    n = 64
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.bin")
+        subprocess.run([b, "gen", "1", "3", "4096", "0", str(n), out], check=True,
+                       env=dict(os.environ, DSM_REF_ROUND_LIMIT=str(1 << 9)))
+        raw = np.fromfile(out, dtype=np.uint8).reshape(n, 32 + 2 * 8 * 64)
+    ref = raw[:, :32].copy().view(orc.RES_DT).reshape(-1)
+    with dsm.Engine(8, 4096) as eng:
+        eng.set_round_limit(9)
+        res, _ = eng.run_generated("hot", 3, 4096, 0, n)
+    _cmp(res, ref)
