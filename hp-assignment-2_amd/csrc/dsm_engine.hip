@@ -28,6 +28,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -209,35 +211,52 @@ DEVI uint4 ld16(const uint16_t *p) {
 
 /* ---- hit-run fast-forward helpers ------------------------------------------------------
  * A trace chunk is 8 packed instructions in 4 dwords (instruction j = half-word j).       */
-/* the 8 instructions starting at half-word s (0..7) of the 16 in (a, b): low 128 bits of
- * (b:a) >> 16 s.  Dword select (3 v_cndmask each) then one v_alignbit per output dword. */
-DEVI void ff_window(const uint32_t (&a)[4], const uint32_t (&b)[4], uint32_t s, uint32_t (&w)[4]) {
-    const uint32_t q = s >> 1, hs = (s & 1u) << 4;
-    const uint32_t d[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    uint32_t t[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j)
-        t[j] = q == 0 ? d[j] : q == 1 ? d[j + 1] : q == 2 ? d[j + 2] : d[j + 3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_alignbit(t[j + 1], t[j], hs);
+/* 128-bit shifts on two 64-bit halves, branch-free (selects and 64-bit shifts only: a
+ * select chain over a per-lane index is turned into divergent branches) */
+DEVI void shr128(uint64_t &lo, uint64_t &hi, uint32_t b) {          /* b = 0..127 */
+    const bool big = b >= 64u;
+    const uint64_t l = big ? hi : lo, h = big ? 0ull : hi;
+    const uint32_t c = b & 63u;
+    lo = (l >> c) | ((h << 1) << (63u - c));
+    hi = h >> c;
 }
-/* x << 16 s (128 bits, zero fill): puts the shift register `cur` (instruction ip at its low
- * half-word) back at its aligned position ip & 7 */
+DEVI void shl128(uint64_t &lo, uint64_t &hi, uint32_t b) {          /* b = 0..128 */
+    const bool big = b >= 64u, none = b >= 128u;
+    const uint64_t h = big ? lo : hi, l = big ? 0ull : lo;
+    const uint32_t c = b & 63u;
+    hi = none ? 0ull : (h << c) | ((l >> 1) >> (63u - c));
+    lo = none ? 0ull : l << c;
+}
+DEVI void to64(const uint32_t (&x)[4], uint64_t &lo, uint64_t &hi) {
+    lo = x[0] | ((uint64_t)x[1] << 32);
+    hi = x[2] | ((uint64_t)x[3] << 32);
+}
+DEVI void from64(uint64_t lo, uint64_t hi, uint32_t (&y)[4]) {
+    y[0] = (uint32_t)lo; y[1] = (uint32_t)(lo >> 32); y[2] = (uint32_t)hi; y[3] = (uint32_t)(hi >> 32);
+}
+/* the 8 instructions starting at half-word s (0..7) of the 16 in (a, b): low 128 bits of
+ * (b:a) >> 16 s */
+DEVI void ff_window(const uint32_t (&a)[4], const uint32_t (&b)[4], uint32_t s, uint32_t (&w)[4]) {
+    uint64_t al, ah, bl, bh;
+    to64(a, al, ah);
+    to64(b, bl, bh);
+    shr128(al, ah, 16u * s);
+    shl128(bl, bh, 128u - 16u * s);
+    from64(al | bl, ah | bh, w);
+}
+/* x << 16 s (128 bits, zero fill), s = 0..8 */
 DEVI void ff_unshift(const uint32_t (&x)[4], uint32_t s, uint32_t (&y)[4]) {
-    const uint32_t q = s >> 1;
-    const bool odd = s & 1u;
-    const uint32_t xz[7] = {0u, 0u, 0u, x[0], x[1], x[2], x[3]};   /* xz[3 + i] = x[i] */
-    uint32_t u[5];                                                 /* u[j + 1] = (x << 32 q)[j] */
-#pragma unroll
-    for (int j = -1; j < 4; ++j)
-        u[j + 1] = j < 0 ? 0u : q == 0 ? xz[3 + j] : q == 1 ? xz[2 + j] : q == 2 ? xz[1 + j] : xz[j];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = odd ? __builtin_amdgcn_alignbit(u[j + 1], u[j], 16) : u[j + 1];
+    uint64_t l, h;
+    to64(x, l, h);
+    shl128(l, h, 16u * s);
+    from64(l, h, y);
 }
 /* x >> 16 s (128 bits, zero fill): the shift-register form of an aligned chunk at ip & 7 = s */
 DEVI void ff_shift(const uint32_t (&x)[4], uint32_t s, uint32_t (&y)[4]) {
-    const uint32_t z[4] = {0u, 0u, 0u, 0u};
-    ff_window(x, z, s, y);
+    uint64_t l, h;
+    to64(x, l, h);
+    shr128(l, h, 16u * s);
+    from64(l, h, y);
 }
 /* GEN: aligned chunk c (instructions 8c .. 8c+7) of the counter-based generator, in the
  * packed-trace layout (gen_instr's key and bit fields) */
@@ -297,6 +316,7 @@ sim_kernel(const SimArgs *Ap) {
      * (not with the issue-order trace or the seeded stalls of schedule exploration) */
     constexpr bool FF = (MODE & (M_TR | M_SX)) == 0;
     constexpr int SW = susp_words(RING);
+    constexpr uint32_t FF_PROBE = 16;   /* fast-forward probe every 16 iterations */
 
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
     __shared__ uint32_t s_line[WAVES][4][64];        /* cache lines: addr | value << 8 | state << 16 */
@@ -417,404 +437,411 @@ sim_kernel(const SimArgs *Ap) {
     }
 
     uint32_t wrounds = 0;    /* loop iterations of this wave (uniform) */
-    uint32_t ffpass = 0, ffiter = 0;   /* fast-forward passes / steps of this wave (uniform) */
+    uint32_t ffpass = 0, ffiter = 0;   /* fast-forward entries (groups) / steps (wave)      */
+    uint64_t ffm = 0;                  /* lanes in fast-forward mode (wave-uniform)          */
     uint64_t liveb = __ballot(live);
-    for (;;) {
-        if (liveb == 0) break;
-        ++wrounds;
-
-        /* ---- (1) this round's action, from state at the start of the round ---------- */
-        /* A dead lane holds an empty inbox and C_WAIT | C_DUMPED, so it never acts.  One
-         * compare gives "inbox empty and not waiting": the count sits at bits 8+ of rh, the
-         * flags at bits 8-11 of ctl.  C_DUMPED there is harmless (a dumped node has issued
-         * every instruction and dumps once), and so are C_OVF / C_ASSERT (their system ends
-         * in the round that sets them). */
-        const uint32_t cnt0 = nd.rh >> 8, head0 = nd.rh & 0xFFu;
-        bool hasMsg = cnt0 != 0;                                          /* :158-169 */
-        const bool canIssue = (nd.rh | nd.ctl) < 256u;                    /* :578-581 */
-        bool doIssue = canIssue && nd.ip < nd.nins;                       /* :590-592 */
-        bool doDump = canIssue && nd.ip >= nd.nins;                       /* :688-697 */
-        bool stall = false;
-        if (SX) {           /* a node with an action may stall this round (dsm_sched_act) */
-            const bool avail = hasMsg || doIssue || doDump;
-            const uint64_t key = (sys << 26) ^ ((uint64_t)(rounds + 1) << 3) ^ (uint64_t)node;
-            const uint32_t h = (uint32_t)(splitmix(smul + key) >> 48);
-            stall = avail && h >= sthr;
-            hasMsg = hasMsg && !stall;
-            doIssue = doIssue && !stall;
-            doDump = doDump && !stall;
-        }
-        /* trace refill: when this round's issue takes the last instruction of `cur`, the
-         * chunk after `nxt` is requested NOW and rotated in at the end of the round, so its
-         * HBM latency overlaps this round's transition and delivery (a load consumed in the
-         * same basic block stalls the whole wave on HBM). */
-        const bool refill = !GEN && doIssue && ((nd.ip + 1) & 7u) == 0 && nd.ip + 1 < nd.nins;
-        uint4 pf;
-        if (refill) pf = ld16(tslot() + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
-        const uint32_t headn = (head0 + 1 == (uint32_t)RING) ? 0u : head0 + 1;
-        nd.rh = hasMsg ? (headn | ((cnt0 - 1) << 8)) : nd.rh;
-        uint32_t w = rmsg;
-        if (doIssue) {
-            uint32_t ins;
-            if (GEN) {
-                ins = gen_instr<NP>(gmul, gdist, gfirst + sys, node, nd.ip);
-            } else {
-                /* `cur` is a 128-bit shift register: the next instruction is its low half-word */
-                ins = cur[0] & 0xFFFFu;
-                cur[0] = __builtin_amdgcn_alignbit(cur[1], cur[0], 16);
-                cur[1] = __builtin_amdgcn_alignbit(cur[2], cur[1], 16);
-                cur[2] = __builtin_amdgcn_alignbit(cur[3], cur[2], 16);
-                cur[3] >>= 16;
-            }
-            w = dt_issue_word(ins);                          /* message-word layout */
-            if (TR) {                  /* the group's issues of this round, in node order */
-                const uint32_t g = (uint32_t)(__ballot(true) >> gbase) & NPM;
-                const uint32_t pos = nev + __builtin_popcount(g & ((1u << node) - 1u));
-                if (pos < Ap->issue_cap) Ap->issue[sys * Ap->issue_cap + pos] = (node << 16) | ins;
-            }
-            nd.ip++;
-        }
-        if (TR) nev += __builtin_popcount((uint32_t)(__ballot(doIssue) >> gbase) & NPM);
-        const uint32_t op = (hasMsg || doIssue) ? dt_type(w) : doDump ? OP_DUMP : OP_IDLE;
-
-        /* ---- (2) decode, then the micro-op table (dsm_table.h) ------------------------ */
-        DtIn in;
-        dt_decode(w, &in.a, &in.v, &in.excl, &in.r2, &in.s);
-        const uint32_t blk = in.a & 15u, idx = in.a & 3u;                  /* :177-184 */
-        uint16_t *const mbp = reinterpret_cast<uint16_t *>(&s_mb[wv][blk >> 1][lane]) + (blk & 1u);
-        const uint32_t mbw = *mbp;
-        in.op = op; in.node = node; in.np_mask = NPM;
-        const uint32_t lw = s_line[wv][idx][lane];
-        in.La = lw & 0xFFu; in.Lv = (lw >> 8) & 0xFFu; in.Ls = lw >> 16;
-        in.Db = mbw >> 8; in.Ds = get2(nd.dst, blk); in.Mv = mbw & 0xFFu; in.pend = nd.ctl & 0xFFu;
-        uint32_t evDb;
-        /* header of op' = dt_opx(in): indexed by op | home << 5 (dt_build's second half
-         * maps EVICT_SHARED at its home to DT_EVSH); with fewer than 8 nodes an instruction
-         * whose home is not simulated is DT_ASSERT */
-        uint32_t hix = op | ((in.a >> 4) == node ? 32u : 0u);
-        if (NP < 8) hix = (op == DT_RD && (in.a >> 4) >= (uint32_t)NP) ? (uint32_t)DT_ASSERT : hix;
-        const uint32_t hdr = reinterpret_cast<const uint32_t *>(&s_tab[DT_ENTRIES])[hix];
-        const uint32_t ti = dt_index(in, hdr, &evDb);
-        const uint2 E = s_tab[ti];
-        /* dt_x / dt_y from the raw words: w = {v, a | x << 7, ..}, lw = {La, Lv, Ls, 0},
-         * mbw = {Mv, Db}, ctl = {pending, ..} */
-        const uint32_t X = __builtin_amdgcn_perm(lw, w, 0x05040001u) & ~0x80u;
-        const uint32_t Y = __builtin_amdgcn_perm(mbw, nd.ctl, 0x0C050400u) | ((evDb & 0xFFu) << 24);
-        const DtOut o = dt_apply_xy(in, X, Y, E.x, E.y, evDb);
-        const uint32_t o0 = o.o0, o1 = o.o1;
-
-        /* ---- (3) write back (idle lanes rewrite unchanged values) ------------------- */
-        s_line[wv][idx][lane] = __builtin_amdgcn_perm(o.S, o.P, 0x0C040100u);   /* nLa nLv nLs */
-        nd.dst = set2(nd.dst, blk, o.nDs);
-        *mbp = (uint16_t)(o.nMv | (o.nDb << 8));
-        nd.ctl = (nd.ctl & ~o.cclr) | o.cset;      /* wait, pendingWriteValue (:633), assert */
-        const bool isMsg = op <= T_EVM;
-        if (FB) nd.nmsg += isMsg ? 1u : 0u;     /* else messages received, counted at delivery */
-        if (TC) {
-            const uint32_t inc = isMsg ? (1u << ((op & 1u) * 16)) : 0u, q = op >> 1;
-#pragma unroll
-            for (uint32_t k = 0; k < 7; ++k) tc[k] += (q == k) ? inc : 0u;
-        }
-        if (doDump) {                                                    /* :688-697 */
-            nd.ctl |= C_DUMPED;               /* printProcessorState(threadId, node), :695 */
-            store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8, nd, s_mb, s_line, wv, lane, 2u);
-        }
-
-        /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        /* the outbox holds ring entries: body | sender << 24 (the masks stay in o0 / o1) */
-        reinterpret_cast<uint2 *>(s_out[wv])[lane] = make_uint2(dt_ring_entry(o0, node), dt_ring_entry(o1, node));
-        /* receive masks, transposed at the sender: word j of this node sets bit 2*node + j of
-         * every destination's mask (LDS atomic OR; a multicast INV visits its destinations in
-         * a short loop), so a receiver reads its mask instead of gathering bits from the
-         * group's destination bytes */
-        {
-            uint32_t m0 = o0 >> 24, m1 = o1 >> 24;
-            uint32_t b0 = 2 * node;            /* recomputed here, not kept in a register */
-            asm volatile("" : "+v"(b0));
-            const uint32_t bit0 = 1u << b0, bit1 = 2u << b0;
-            if (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
-            if (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
-            while (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
-            while (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        uint32_t R = s_rm[wv][lane];     /* bit 2*sender+word: that word is addressed to me */
-        s_rm[wv][lane] = 0;
-        /* the fast kernel counts messages received (handled = received - still in the ring,
-         * taken at the finish); an overflow is flagged here and set in ctl on the finish
-         * path, where its system ends */
-        if (!FB)      /* one v_bcnt with its accumulator (the compiler would share the count) */
-            asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(nd.nmsg) : "v"(R));
-        uint32_t nccv;
-        {
-            /* appended at the tail in R's bit order.  An overflowing ring sets C_OVF and its
-             * tail wraps onto live entries: the system ends this round (the transition
-             * kernel hands it to the 256-deep re-run, which reports RING_OVERFLOW), and the
-             * ring is not part of any record or result. */
-            const uint32_t hh = nd.rh & 0xFFu, cc = nd.rh >> 8;
-            const uint32_t ncc = cc + __builtin_popcount(R);
-            nccv = ncc;
-            uint32_t slot = hh + cc;
-            slot = slot >= (uint32_t)RING ? slot - RING : slot;
-            while (R) {
-                const uint32_t j = __builtin_ctz(R);
-                R &= R - 1;
-                s_ring[wv][slot][lane] = s_out[wv][2 * gbase + j];
-                slot = (slot + 1 == (uint32_t)RING) ? 0u : slot + 1;
-            }
-            nd.rh = hh | ((ncc < (uint32_t)RING ? ncc : (uint32_t)RING) << 8);
-            rmsg = s_ring[wv][hh][lane];          /* next round's head, prefetched */
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        if (refill) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-            nxt[0] = pf.x; nxt[1] = pf.y; nxt[2] = pf.z; nxt[3] = pf.w;
-        }
-
-        /* ---- (4b) hit-run fast-forward (exact) ----------------------------------------- *
-         * After a round in which a system sent nothing (every node issued a hit -- RD hit,
-         * :607-611; WR hit on M/E, :635-645 -- or idled), every inbox of it is empty, and
-         * until some node issues an instruction that sends, nothing reaches any node: each
-         * round is then one more local hit per non-waiting node (a waiting node stays idle,
-         * :578-581).  A hit never changes which later instructions hit (only E -> M, and
-         * values), so each issuing node's run of hits is fixed by its trace and its 4 line
-         * tags.  The group applies the next k rounds at once, k = the minimum run over its
-         * issuing nodes, 8 instructions per step: per node the last value written to each
-         * line (state M), pendingWriteValue (:633) and the instruction index, and
-         * rounds += k.  A node with instructions left but not yet dumped, or the round
-         * limit, bounds k; the round that breaks the run runs normally. */
-        if (FF) {
-            const bool quiet = (op == OP_RD || op == OP_IDLE) &&
-                               (((o0 | o1) >> 24) | (nd.ctl & C_ASSERT)) == 0u;
-            const uint64_t hitb = __ballot(quiet && op == OP_RD);
-            if (hitb) {
-                const uint64_t qb = __ballot(quiet);
-                const bool ffa = live && ((qb >> gbase) & NPM) == NPM && ((hitb >> gbase) & NPM) != 0;
-                if (__ballot(ffa)) {
-                    ++ffpass;
-                    const bool iss = ffa && (nd.ctl & C_WAIT) == 0u && nd.ip < nd.nins;
-                    const bool dpend = ffa && (nd.ctl & (C_WAIT | C_DUMPED)) == 0u && nd.ip >= nd.nins;
+    /* one lock-step round of every system of the wave; compiled twice: with the
+     * fast-forward step and its gating (WFF, while some group of the wave is in
+     * fast-forward mode) and without (the plain round the wave runs otherwise) */
+    auto round = [&](auto wff) {
+        constexpr bool WFF = FF && decltype(wff)::value;
+            if (WFF) {
+                /* ---- (0) hit-run fast-forward (exact) -------------------------------------- *
+                 * When every inbox of a system is empty, nothing reaches any of its nodes until
+                 * one of them issues an instruction that sends: each round is one more local hit
+                 * per non-waiting node (RD hit :607-611, WR hit on M/E :635-645; a waiting node
+                 * stays idle, :578-581).  A hit never changes which later instructions hit (only
+                 * E -> M and values), so each issuing node's run of hits is fixed by its trace
+                 * and its 4 line tags.  A group in fast-forward mode applies the next k rounds
+                 * at once each iteration, k = the minimum run over its issuing nodes within their
+                 * next 8 instructions: per node the last value written to each line (state M),
+                 * pendingWriteValue (:633) and the instruction index, rounds += k.  A node with
+                 * its trace done but not yet dumped, no issuing node, or the round limit bound
+                 * k; at k < 8 the group leaves the mode and runs this iteration's round normally
+                 * (the one that breaks the run).  The shift register cur / nxt keeps its meaning,
+                 * so the mode has no state but the wave's lane mask. */
+                const bool inff = __builtin_amdgcn_inverse_ballot_w64(ffm);
+                ++ffiter;
+                uint32_t k = 8;
+                if (inff) {
+                    const bool iss = (nd.ctl & C_WAIT) == 0u && nd.ip < nd.nins;
+                    const bool dpend = (nd.ctl & (C_WAIT | C_DUMPED)) == 0u && nd.ip >= nd.nins;
                     /* line tags for a hit: RD needs a valid line, WR a line in M or E */
                     uint32_t kr = 0, kw = 0;
-#pragma unroll
+    #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const uint32_t lw = s_line[wv][i][lane];
                         const uint32_t la = lw & 0xFFu, ls = lw >> 16;
                         kr |= (ls != DT_CI ? la : 0xFFu) << (8 * i);
                         kw |= (ls <= DT_CE ? la : 0xFFu) << (8 * i);
                     }
-                    uint32_t A[4], B[4], P[4] = {0u, 0u, 0u, 0u};
+                    const uint32_t s = nd.ip & 7u, m = 8u - s;
+                    uint32_t W[4];
                     if (GEN) {
+                        uint32_t A[4], B[4];
                         gen_chunk<NP>(gmul, gdist, gfirst + sys, node, nd.ip >> 3, A);
                         gen_chunk<NP>(gmul, gdist, gfirst + sys, node, (nd.ip >> 3) + 1, B);
-                    } else {
-                        ff_unshift(cur, nd.ip & 7u, A);
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) B[q] = nxt[q];
+                        ff_window(A, B, s, W);
+                    } else {        /* the next 8: cur's m, then nxt's first s */
+                        uint32_t T[4];
+                        ff_unshift(nxt, m, T);
+    #pragma unroll
+                        for (int q = 0; q < 4; ++q) W[q] = cur[q] | T[q];
                     }
-                    /* little state across the loop (the kernel runs at its VGPR budget):
-                     * the window's aligned chunks A, B and the prefetch P, the line tags,
-                     * the values written per line; ip, pendingWriteValue and rounds are
-                     * updated in place */
-                    uint32_t lval = 0, wm = 0;
-                    bool act = ffa;
-                    for (;;) {
-                        if (__ballot(act) == 0) break;
-                        ++ffiter;
-                        if (act) {
-                            const uint32_t c = nd.ip >> 3, s = nd.ip & 7u;
-                            if (iss) {          /* next chunk in flight during the scan */
-                                if (GEN) {
-                                    gen_chunk<NP>(gmul, gdist, gfirst + sys, node, c + 2, P);
-                                } else {
-                                    const uint32_t pc = (c + 2) * 8u + 8u <= stride ? (c + 2) * 8u : stride - 8u;
-                                    const uint4 v = ld16(tslot() + pc);
-                                    P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
-                                }
-                            }
-                            uint32_t W[4];
-                            ff_window(A, B, s, W);
-                            uint32_t hm = 0;
-#pragma unroll
-                            for (int j = 0; j < 8; ++j) {
-                                const uint32_t h = (W[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                                const uint32_t key = (h & 0x8000u) ? kw : kr;
-                                const uint32_t tag = __builtin_amdgcn_ubfe(key, (h >> 5) & 0x18u, 8);
-                                hm |= (tag == ((h >> 8) & 0x7Fu)) ? (1u << j) : 0u;
-                            }
-                            uint32_t r = iss ? (uint32_t)__builtin_ctz(~hm) : (dpend ? 0u : 8u);
-                            if (iss && r > nd.nins - nd.ip) r = nd.nins - nd.ip;
-                            const uint32_t left = lim - 1u - rounds;   /* round limit */
-                            if (r > left) r = left;
-                            const uint32_t k = gmin<NP>(r);
-                            if (iss) {
-#pragma unroll
-                                for (int j = 0; j < 8; ++j) {
-                                    const uint32_t h = (W[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                                    if ((uint32_t)j < k && (h & 0x8000u)) {   /* WR hit :633, :640-645 */
-                                        const uint32_t sh = (h >> 5) & 0x18u;
-                                        lval = (lval & ~(0xFFu << sh)) | ((h & 0xFFu) << sh);
-                                        wm |= 1u << (sh >> 3);
-                                        nd.ctl = (nd.ctl & ~0xFFu) | (h & 0xFFu);
-                                    }
-                                }
-                                nd.ip += k;
-                            }
-                            rounds += k;
-                            if (k < 8u) {
-                                act = false;
-                                if (!GEN) {
-                                    /* shift register and next chunk at the (new) ip, rebuilt
-                                     * from the window's chunks (a node that did not issue gets
-                                     * its own back), so cur / nxt are dead across the loop */
-                                    const bool cross = s + (iss ? k : 0u) >= 8u;
-                                    uint32_t X[4];
-#pragma unroll
-                                    for (int q = 0; q < 4; ++q) X[q] = cross ? B[q] : A[q];
-                                    ff_shift(X, nd.ip & 7u, cur);
-#pragma unroll
-                                    for (int q = 0; q < 4; ++q) nxt[q] = cross ? P[q] : B[q];
-                                }
-                            } else if (iss) {      /* the others keep their chunks */
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) { A[q] = B[q]; B[q] = P[q]; }
+                    uint32_t hm = 0;
+    #pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t h = (W[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                        const uint32_t key = (h & 0x8000u) ? kw : kr;
+                        const uint32_t tag = __builtin_amdgcn_ubfe(key, (h >> 5) & 0x18u, 8);
+                        hm |= (tag == ((h >> 8) & 0x7Fu)) ? (1u << j) : 0u;
+                    }
+                    /* a group with no node issuing makes no progress here */
+                    const bool gany = ((__ballot(iss) >> gbase) & NPM) != 0u;
+                    uint32_t r = iss ? (uint32_t)__builtin_ctz(~hm) : (dpend || !gany ? 0u : 8u);
+                    if (iss && r > nd.nins - nd.ip) r = nd.nins - nd.ip;
+                    /* the round limit: the round that reaches it runs normally */
+                    if (r > lim - 1u - rounds) r = lim - 1u - rounds;
+                    k = gmin<NP>(r);
+                    if (iss && k) {
+                        uint32_t lval = 0, wm = 0;
+    #pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const uint32_t h = (W[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                            if ((uint32_t)j < k && (h & 0x8000u)) {   /* WR hit :633, :640-645 */
+                                const uint32_t sh = (h >> 5) & 0x18u;
+                                lval = (lval & ~(0xFFu << sh)) | ((h & 0xFFu) << sh);
+                                wm |= 1u << (sh >> 3);
+                                nd.ctl = (nd.ctl & ~0xFFu) | (h & 0xFFu);
                             }
                         }
-                    }
-                    if (iss) {
-#pragma unroll
+    #pragma unroll
                         for (int i = 0; i < 4; ++i)
                             if ((wm >> i) & 1u) {   /* value written, state MODIFIED (0) */
                                 const uint32_t lw = s_line[wv][i][lane];
                                 s_line[wv][i][lane] = (lw & 0xFFu) | (((lval >> (8 * i)) & 0xFFu) << 8);
                             }
-                    }
-                }
-            }
-        }
-
-        /* ---- (5) per-system termination (Appendix A step 4) -------------------------- *
-         * A round in which no node of a system acts changes nothing, so every later round
-         * is idle too: the active rounds of a system are a prefix, and `rounds` counts every
-         * round, less the final idle one.  The per-round test is wave-uniform: a live group
-         * with no active lane (a zero field in actb | ~liveb), or a lane with an assert, an
-         * overflow or the round limit; the per-lane finish runs only then. */
-        ++rounds;
-        /* both tests on VGPR integers (one compare each; the round limit is a power of two) */
-        uint32_t opv = op;
-        asm volatile("" : "+v"(opv));
-        const uint64_t actb = __ballot(opv != OP_IDLE || stall);   /* stalled = available */
-        /* rounds >> rsh: the round limit, or the budget pass's 1 << rsh */
-        const uint64_t flagb = __ballot(((nd.ctl & C_ASSERT) | (rounds >> rsh)) != 0u) |
-                               __ballot(nccv > ocap);
-        constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
-        constexpr uint64_t GHI = GLO << (NP - 1);
-        const uint64_t t = actb | ~liveb;
-        if ((((t - GLO) & ~t & GHI) | (flagb & liveb)) == 0) continue;
-        if (nccv > ocap) nd.ctl |= C_OVF;
-        const uint32_t gact = (uint32_t)(actb >> gbase) & NPM;
-        const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
-        const bool gbad = ((badb >> gbase) & NPM) != 0;
-        if (gact == 0) --rounds;
-        /* budget pass: a system still running after 1 << rsh rounds is suspended */
-        const bool susp = budget && gact != 0 && !gbad && rounds >= (1u << rsh) && rounds < lim;
-        const bool done = live && (gact == 0 || gbad || rounds >= lim || susp);
-
-        const uint64_t doneb = __ballot(done);
-        if (doneb) {
-            const uint64_t dumpb = __ballot((nd.ctl & C_DUMPED) != 0u);
-            const uint64_t asrb = __ballot((nd.ctl & C_ASSERT) != 0u);
-            if (done) {
-                const uint32_t dmask = (uint32_t)(dumpb >> gbase) & NPM;
-                const bool gasr = ((asrb >> gbase) & NPM) != 0;
-                uint32_t st;
-                if (gasr) st = DSM_ASSERT_FAILED;
-                else if (gbad) st = DSM_RING_OVERFLOW;
-                else if (gact == 0) st = (dmask == NPM) ? DSM_COMPLETED : DSM_DEADLOCKED;
-                else st = DSM_ROUND_LIMIT;
-                const bool handoff = !FB && (st == DSM_RING_OVERFLOW);
-                const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
-                if (!handoff && !susp) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
-                if (susp) {               /* save the node for the resume pass (start()) */
-                    uint32_t *sp = Ap->susp + sys * (uint64_t)(SW * NP) + node;
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) sp[i * NP] = s_mb[wv][i][lane];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) sp[(8 + i) * NP] = s_line[wv][i][lane];
-#pragma unroll
-                    for (int i = 0; i < RING; ++i) sp[(12 + i) * NP] = s_ring[wv][i][lane];
-                    uint32_t *q = sp + (12 + RING) * NP;
-                    q[0] = nd.dst; q[NP] = nd.ctl; q[2 * NP] = nd.ip; q[3 * NP] = nd.nins;
-                    q[4 * NP] = nd.rh; q[5 * NP] = nd.nmsg; q[6 * NP] = rounds;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) { q[(7 + k) * NP] = cur[k]; q[(11 + k) * NP] = nxt[k]; }
-                }
-                const uint32_t ins = gsum32<NP>(nd.ip), msgs = gsum32<NP>(nd.nmsg - (FB ? 0u : nd.rh >> 8));
-                uint32_t nlo = 0xFFFFFFFFu, nhi = 0xFFFFFFFFu;
-                if (node == 0) {
-                    if (susp) {
-                        const uint32_t pos = atomicAdd(Ap->susp_count, 1u);
-                        Ap->susp_list[pos] = (uint32_t)sys;
-                        atomicAdd(&s_cnt[wv][K_RESUMED], 1ull);
-                    } else if (handoff) {
-                        const uint32_t pos = atomicAdd(Ap->ovf_count, 1u);
-                        Ap->ovf_list[pos] = (uint32_t)sys;
-                        atomicAdd(&s_cnt[wv][K_OVFRERUN], 1ull);
-                    } else {
-                        reinterpret_cast<uint4 *>(Ap->results)[2 * sys] =
-                            make_uint4(st | (dmask << 8), rounds, msgs, ins);
-                        if (TR) Ap->issue_n[sys] = nev;
-                        atomicAdd(&s_cnt[wv][K_MSGS], (unsigned long long)msgs);
-                        atomicAdd(&s_cnt[wv][K_INSTRS], (unsigned long long)ins);
-                        atomicAdd(&s_cnt[wv][K_ROUNDS], (unsigned long long)rounds);
-                        atomicAdd(&s_cnt[wv][K_SYSTEMS], 1ull);
-                        atomicAdd(&s_cnt[wv][K_STATUS + st], 1ull);
-                        atomicMax(&s_cnt[wv][K_MAXR], (unsigned long long)rounds);
-                    }
-                    /* next system: static first assignment, then 8 sharded counters */
-                    const uint64_t rs = n > pool ? (n - pool + 7) / 8 : 0;
-                    while (tried < 8) {
-                        const uint64_t lo = pool + (uint64_t)shard * rs;
-                        const uint64_t len = (n > lo) ? ((n - lo) < rs ? (n - lo) : rs) : 0;
-                        if (len) {
-                            const uint32_t r = atomicAdd(&Ap->claim[shard * 32u], 1u);
-                            if (r < len) {
-                                const uint64_t nl = lo + r;
-                                nlo = (uint32_t)nl; nhi = (uint32_t)(nl >> 32);
-                                break;
+                        if (!GEN) {     /* consume k from the shift register cur ++ nxt */
+                            const bool cross = k >= m;
+                            uint32_t X[4];
+    #pragma unroll
+                            for (int q = 0; q < 4; ++q) X[q] = cross ? nxt[q] : cur[q];
+                            ff_shift(X, cross ? k - m : k, cur);
+                            if (cross) {   /* the chunk after: used next iteration at the earliest */
+                                const uint32_t pc = ((nd.ip >> 3) + 2) * 8u;
+                                const uint4 v = ld16(tslot() + (pc + 8u <= stride ? pc : stride - 8u));
+                                nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
                             }
                         }
-                        shard = (shard + 1) & 7u;
-                        ++tried;
+                        nd.ip += k;
                     }
+                    rounds += k;
                 }
-                if (TC && !handoff) {
-#pragma unroll
-                    for (uint32_t t = 0; t < DSM_NTYPES; ++t) {
-                        const uint32_t c = (tc[t >> 1] >> ((t & 1u) * 16)) & 0xFFFFu;
-                        if (c) atomicAdd(&s_cnt[wv][t], (unsigned long long)c);
-                    }
-                }
-                nlo = __shfl(nlo, (int)gbase, 64);
-                nhi = __shfl(nhi, (int)gbase, 64);
-                const uint64_t nl = ((uint64_t)nhi << 32) | nlo;
-                if (nl != NO_SYS) {
-                    start(nl);
+                ffpass += (uint32_t)__builtin_popcountll(__ballot(inff && node == 0u && k != 0u));
+                ffm &= ~__ballot(inff && k < 8u);   /* those run this iteration's round normally */
+            }
+            /* still in the mode: no round here (the lane's bit of the wave-uniform mask) */
+            const bool inff = WFF && __builtin_amdgcn_inverse_ballot_w64(ffm);
+            uint32_t op = OP_IDLE, o0 = 0, o1 = 0, nccv = nd.rh >> 8;
+            bool stall = false;
+            if (!WFF || (liveb & ~ffm) != 0) {
+            /* ---- (1) this round's action, from state at the start of the round ---------- */
+            /* A dead lane holds an empty inbox and C_WAIT | C_DUMPED, so it never acts.  One
+             * compare gives "inbox empty and not waiting": the count sits at bits 8+ of rh, the
+             * flags at bits 8-11 of ctl.  C_DUMPED there is harmless (a dumped node has issued
+             * every instruction and dumps once), and so are C_OVF / C_ASSERT (their system ends
+             * in the round that sets them).  A node in fast-forward mode has an empty inbox and
+             * takes no action here. */
+            const uint32_t cnt0 = nd.rh >> 8, head0 = nd.rh & 0xFFu;
+            bool hasMsg = cnt0 != 0;                                          /* :158-169 */
+            const bool canIssue = (nd.rh | nd.ctl) < 256u && !inff;           /* :578-581 */
+            bool doIssue = canIssue && nd.ip < nd.nins;                       /* :590-592 */
+            bool doDump = canIssue && nd.ip >= nd.nins;                       /* :688-697 */
+            if (SX) {           /* a node with an action may stall this round (dsm_sched_act) */
+                const bool avail = hasMsg || doIssue || doDump;
+                const uint64_t key = (sys << 26) ^ ((uint64_t)(rounds + 1) << 3) ^ (uint64_t)node;
+                const uint32_t h = (uint32_t)(splitmix(smul + key) >> 48);
+                stall = avail && h >= sthr;
+                hasMsg = hasMsg && !stall;
+                doIssue = doIssue && !stall;
+                doDump = doDump && !stall;
+            }
+            /* trace refill: when this round's issue takes the last instruction of `cur`, the
+             * chunk after `nxt` is requested NOW and rotated in at the end of the round, so its
+             * HBM latency overlaps this round's transition and delivery (a load consumed in the
+             * same basic block stalls the whole wave on HBM). */
+            const bool refill = !GEN && doIssue && ((nd.ip + 1) & 7u) == 0 && nd.ip + 1 < nd.nins;
+            uint4 pf;
+            if (refill) pf = ld16(tslot() + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
+            const uint32_t headn = (head0 + 1 == (uint32_t)RING) ? 0u : head0 + 1;
+            nd.rh = hasMsg ? (headn | ((cnt0 - 1) << 8)) : nd.rh;
+            uint32_t w = rmsg;
+            if (doIssue) {
+                uint32_t ins;
+                if (GEN) {
+                    ins = gen_instr<NP>(gmul, gdist, gfirst + sys, node, nd.ip);
                 } else {
-                    live = false;
-                    nd.rh = 0;
-                    nd.ctl = C_WAIT | C_DUMPED;      /* never acts again (round step (1)) */
+                    /* `cur` is a 128-bit shift register: the next instruction is its low half-word */
+                    ins = cur[0] & 0xFFFFu;
+                    cur[0] = __builtin_amdgcn_alignbit(cur[1], cur[0], 16);
+                    cur[1] = __builtin_amdgcn_alignbit(cur[2], cur[1], 16);
+                    cur[2] = __builtin_amdgcn_alignbit(cur[3], cur[2], 16);
+                    cur[3] >>= 16;
+                }
+                w = dt_issue_word(ins);                          /* message-word layout */
+                if (TR) {                  /* the group's issues of this round, in node order */
+                    const uint32_t g = (uint32_t)(__ballot(true) >> gbase) & NPM;
+                    const uint32_t pos = nev + __builtin_popcount(g & ((1u << node) - 1u));
+                    if (pos < Ap->issue_cap) Ap->issue[sys * Ap->issue_cap + pos] = (node << 16) | ins;
+                }
+                nd.ip++;
+            }
+            if (TR) nev += __builtin_popcount((uint32_t)(__ballot(doIssue) >> gbase) & NPM);
+            op = (hasMsg || doIssue) ? dt_type(w) : doDump ? OP_DUMP : OP_IDLE;
+
+            /* ---- (2) decode, then the micro-op table (dsm_table.h) ------------------------ */
+            DtIn in;
+            dt_decode(w, &in.a, &in.v, &in.excl, &in.r2, &in.s);
+            const uint32_t blk = in.a & 15u, idx = in.a & 3u;                  /* :177-184 */
+            uint16_t *const mbp = reinterpret_cast<uint16_t *>(&s_mb[wv][blk >> 1][lane]) + (blk & 1u);
+            const uint32_t mbw = *mbp;
+            in.op = op; in.node = node; in.np_mask = NPM;
+            const uint32_t lw = s_line[wv][idx][lane];
+            in.La = lw & 0xFFu; in.Lv = (lw >> 8) & 0xFFu; in.Ls = lw >> 16;
+            in.Db = mbw >> 8; in.Ds = get2(nd.dst, blk); in.Mv = mbw & 0xFFu; in.pend = nd.ctl & 0xFFu;
+            uint32_t evDb;
+            /* header of op' = dt_opx(in): indexed by op | home << 5 (dt_build's second half
+             * maps EVICT_SHARED at its home to DT_EVSH); with fewer than 8 nodes an instruction
+             * whose home is not simulated is DT_ASSERT */
+            uint32_t hix = op | ((in.a >> 4) == node ? 32u : 0u);
+            if (NP < 8) hix = (op == DT_RD && (in.a >> 4) >= (uint32_t)NP) ? (uint32_t)DT_ASSERT : hix;
+            const uint32_t hdr = reinterpret_cast<const uint32_t *>(&s_tab[DT_ENTRIES])[hix];
+            const uint32_t ti = dt_index(in, hdr, &evDb);
+            const uint2 E = s_tab[ti];
+            /* dt_x / dt_y from the raw words: w = {v, a | x << 7, ..}, lw = {La, Lv, Ls, 0},
+             * mbw = {Mv, Db}, ctl = {pending, ..} */
+            const uint32_t X = __builtin_amdgcn_perm(lw, w, 0x05040001u) & ~0x80u;
+            const uint32_t Y = __builtin_amdgcn_perm(mbw, nd.ctl, 0x0C050400u) | ((evDb & 0xFFu) << 24);
+            const DtOut o = dt_apply_xy(in, X, Y, E.x, E.y, evDb);
+            o0 = o.o0; o1 = o.o1;
+
+            /* ---- (3) write back (idle lanes rewrite unchanged values) ------------------- */
+            s_line[wv][idx][lane] = __builtin_amdgcn_perm(o.S, o.P, 0x0C040100u);   /* nLa nLv nLs */
+            nd.dst = set2(nd.dst, blk, o.nDs);
+            *mbp = (uint16_t)(o.nMv | (o.nDb << 8));
+            nd.ctl = (nd.ctl & ~o.cclr) | o.cset;      /* wait, pendingWriteValue (:633), assert */
+            const bool isMsg = op <= T_EVM;
+            if (FB) nd.nmsg += isMsg ? 1u : 0u;     /* else messages received, counted at delivery */
+            if (TC) {
+                const uint32_t inc = isMsg ? (1u << ((op & 1u) * 16)) : 0u, q = op >> 1;
+    #pragma unroll
+                for (uint32_t k = 0; k < 7; ++k) tc[k] += (q == k) ? inc : 0u;
+            }
+            if (doDump) {                                                    /* :688-697 */
+                nd.ctl |= C_DUMPED;               /* printProcessorState(threadId, node), :695 */
+                store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8, nd, s_mb, s_line, wv, lane, 2u);
+            }
+
+            /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            /* the outbox holds ring entries: body | sender << 24 (the masks stay in o0 / o1) */
+            reinterpret_cast<uint2 *>(s_out[wv])[lane] = make_uint2(dt_ring_entry(o0, node), dt_ring_entry(o1, node));
+            /* receive masks, transposed at the sender: word j of this node sets bit 2*node + j of
+             * every destination's mask (LDS atomic OR; a multicast INV visits its destinations in
+             * a short loop), so a receiver reads its mask instead of gathering bits from the
+             * group's destination bytes */
+            {
+                uint32_t m0 = o0 >> 24, m1 = o1 >> 24;
+                uint32_t b0 = 2 * node;            /* recomputed here, not kept in a register */
+                asm volatile("" : "+v"(b0));
+                const uint32_t bit0 = 1u << b0, bit1 = 2u << b0;
+                if (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
+                if (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
+                while (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
+                while (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            uint32_t R = s_rm[wv][lane];     /* bit 2*sender+word: that word is addressed to me */
+            s_rm[wv][lane] = 0;
+            /* the fast kernel counts messages received (handled = received - still in the ring,
+             * taken at the finish); an overflow is flagged here and set in ctl on the finish
+             * path, where its system ends */
+            if (!FB)      /* one v_bcnt with its accumulator (the compiler would share the count) */
+                asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(nd.nmsg) : "v"(R));
+            {
+                /* appended at the tail in R's bit order.  An overflowing ring sets C_OVF and its
+                 * tail wraps onto live entries: the system ends this round (the transition
+                 * kernel hands it to the 256-deep re-run, which reports RING_OVERFLOW), and the
+                 * ring is not part of any record or result. */
+                const uint32_t hh = nd.rh & 0xFFu, cc = nd.rh >> 8;
+                const uint32_t ncc = cc + __builtin_popcount(R);
+                nccv = ncc;
+                uint32_t slot = hh + cc;
+                slot = slot >= (uint32_t)RING ? slot - RING : slot;
+                while (R) {
+                    const uint32_t j = __builtin_ctz(R);
+                    R &= R - 1;
+                    s_ring[wv][slot][lane] = s_out[wv][2 * gbase + j];
+                    slot = (slot + 1 == (uint32_t)RING) ? 0u : slot + 1;
+                }
+                nd.rh = hh | ((ncc < (uint32_t)RING ? ncc : (uint32_t)RING) << 8);
+                rmsg = s_ring[wv][hh][lane];          /* next round's head, prefetched */
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            if (refill) {
+    #pragma unroll
+                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+                nxt[0] = pf.x; nxt[1] = pf.y; nxt[2] = pf.z; nxt[3] = pf.w;
+            }
+
+            }   /* normal round */
+
+            /* ---- (5) per-system termination (Appendix A step 4) -------------------------- *
+             * A round in which no node of a system acts changes nothing, so every later round
+             * is idle too: the active rounds of a system are a prefix, and `rounds` counts every
+             * round, less the final idle one.  The per-round test is wave-uniform: a live group
+             * with no active lane (a zero field in actb | ~liveb), or a lane with an assert, an
+             * overflow or the round limit; the per-lane finish runs only then.  A group in
+             * fast-forward mode counted its rounds in step (4b) and is active. */
+            if (!inff) ++rounds;
+            /* both tests on VGPR integers (one compare each; the round limit is a power of two) */
+            uint32_t opv = op;
+            asm volatile("" : "+v"(opv));
+            const uint64_t actb = __ballot(opv != OP_IDLE || stall) | (WFF ? ffm : 0ull);
+            /* rounds >> rsh: the round limit, or the budget pass's 1 << rsh */
+            const uint64_t flagb = __ballot(((nd.ctl & C_ASSERT) | (rounds >> rsh)) != 0u) |
+                                   __ballot(nccv > ocap);
+            constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
+            constexpr uint64_t GHI = GLO << (NP - 1);
+            const uint64_t t = actb | ~liveb;
+            if ((((t - GLO) & ~t & GHI) | (flagb & liveb)) == 0) return;
+            if (nccv > ocap) nd.ctl |= C_OVF;
+            const uint32_t gact = (uint32_t)(actb >> gbase) & NPM;
+            const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
+            const bool gbad = ((badb >> gbase) & NPM) != 0;
+            if (gact == 0) --rounds;
+            /* budget pass: a system still running after 1 << rsh rounds is suspended */
+            const bool susp = budget && gact != 0 && !gbad && rounds >= (1u << rsh) && rounds < lim;
+            const bool done = live && (gact == 0 || gbad || rounds >= lim || susp);
+
+            const uint64_t doneb = __ballot(done);
+            if (doneb) {
+                if (FF) ffm &= ~doneb;        /* the slot's next system starts normally */
+                const uint64_t dumpb = __ballot((nd.ctl & C_DUMPED) != 0u);
+                const uint64_t asrb = __ballot((nd.ctl & C_ASSERT) != 0u);
+                if (done) {
+                    const uint32_t dmask = (uint32_t)(dumpb >> gbase) & NPM;
+                    const bool gasr = ((asrb >> gbase) & NPM) != 0;
+                    uint32_t st;
+                    if (gasr) st = DSM_ASSERT_FAILED;
+                    else if (gbad) st = DSM_RING_OVERFLOW;
+                    else if (gact == 0) st = (dmask == NPM) ? DSM_COMPLETED : DSM_DEADLOCKED;
+                    else st = DSM_ROUND_LIMIT;
+                    const bool handoff = !FB && (st == DSM_RING_OVERFLOW);
+                    const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
+                    if (!handoff && !susp) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
+                    if (susp) {               /* save the node for the resume pass (start()) */
+                        uint32_t *sp = Ap->susp + sys * (uint64_t)(SW * NP) + node;
+    #pragma unroll
+                        for (int i = 0; i < 8; ++i) sp[i * NP] = s_mb[wv][i][lane];
+    #pragma unroll
+                        for (int i = 0; i < 4; ++i) sp[(8 + i) * NP] = s_line[wv][i][lane];
+    #pragma unroll
+                        for (int i = 0; i < RING; ++i) sp[(12 + i) * NP] = s_ring[wv][i][lane];
+                        uint32_t *q = sp + (12 + RING) * NP;
+                        q[0] = nd.dst; q[NP] = nd.ctl; q[2 * NP] = nd.ip; q[3 * NP] = nd.nins;
+                        q[4 * NP] = nd.rh; q[5 * NP] = nd.nmsg; q[6 * NP] = rounds;
+    #pragma unroll
+                        for (int k = 0; k < 4; ++k) { q[(7 + k) * NP] = cur[k]; q[(11 + k) * NP] = nxt[k]; }
+                    }
+                    const uint32_t ins = gsum32<NP>(nd.ip), msgs = gsum32<NP>(nd.nmsg - (FB ? 0u : nd.rh >> 8));
+                    uint32_t nlo = 0xFFFFFFFFu, nhi = 0xFFFFFFFFu;
+                    if (node == 0) {
+                        if (susp) {
+                            const uint32_t pos = atomicAdd(Ap->susp_count, 1u);
+                            Ap->susp_list[pos] = (uint32_t)sys;
+                            atomicAdd(&s_cnt[wv][K_RESUMED], 1ull);
+                        } else if (handoff) {
+                            const uint32_t pos = atomicAdd(Ap->ovf_count, 1u);
+                            Ap->ovf_list[pos] = (uint32_t)sys;
+                            atomicAdd(&s_cnt[wv][K_OVFRERUN], 1ull);
+                        } else {
+                            reinterpret_cast<uint4 *>(Ap->results)[2 * sys] =
+                                make_uint4(st | (dmask << 8), rounds, msgs, ins);
+                            if (TR) Ap->issue_n[sys] = nev;
+                            atomicAdd(&s_cnt[wv][K_MSGS], (unsigned long long)msgs);
+                            atomicAdd(&s_cnt[wv][K_INSTRS], (unsigned long long)ins);
+                            atomicAdd(&s_cnt[wv][K_ROUNDS], (unsigned long long)rounds);
+                            atomicAdd(&s_cnt[wv][K_SYSTEMS], 1ull);
+                            atomicAdd(&s_cnt[wv][K_STATUS + st], 1ull);
+                            atomicMax(&s_cnt[wv][K_MAXR], (unsigned long long)rounds);
+                        }
+                        /* next system: static first assignment, then 8 sharded counters */
+                        const uint64_t rs = n > pool ? (n - pool + 7) / 8 : 0;
+                        while (tried < 8) {
+                            const uint64_t lo = pool + (uint64_t)shard * rs;
+                            const uint64_t len = (n > lo) ? ((n - lo) < rs ? (n - lo) : rs) : 0;
+                            if (len) {
+                                const uint32_t r = atomicAdd(&Ap->claim[shard * 32u], 1u);
+                                if (r < len) {
+                                    const uint64_t nl = lo + r;
+                                    nlo = (uint32_t)nl; nhi = (uint32_t)(nl >> 32);
+                                    break;
+                                }
+                            }
+                            shard = (shard + 1) & 7u;
+                            ++tried;
+                        }
+                    }
+                    if (TC && !handoff) {
+    #pragma unroll
+                        for (uint32_t t = 0; t < DSM_NTYPES; ++t) {
+                            const uint32_t c = (tc[t >> 1] >> ((t & 1u) * 16)) & 0xFFFFu;
+                            if (c) atomicAdd(&s_cnt[wv][t], (unsigned long long)c);
+                        }
+                    }
+                    nlo = __shfl(nlo, (int)gbase, 64);
+                    nhi = __shfl(nhi, (int)gbase, 64);
+                    const uint64_t nl = ((uint64_t)nhi << 32) | nlo;
+                    if (nl != NO_SYS) {
+                        start(nl);
+                    } else {
+                        live = false;
+                        nd.rh = 0;
+                        nd.ctl = C_WAIT | C_DUMPED;      /* never acts again (round step (1)) */
+                    }
                 }
             }
+            const uint64_t nlive = __ballot(live);
+            /* budget pass: once a slot of this wave found no new system, the wave's remaining
+             * systems get the late budget, so the launch's tail is not a system claimed last
+             * running its full budget at falling occupancy (the resume pass continues them) */
+            if (budget && late_rsh && (liveb & ~nlive)) rsh = late_rsh < rsh ? late_rsh : rsh;
+            liveb = nlive;
+    };
+
+    for (;;) {
+        if (liveb == 0) break;
+        ++wrounds;
+
+        /* FF: lanes of groups in fast-forward mode do one fast-forward step (0) this
+         * iteration instead of a normal round; when every live lane is in that mode the
+         * normal round is skipped altogether */
+        if (FF && (wrounds & (FF_PROBE - 1u)) == 0u) {
+            /* probe: every group whose inboxes are all empty tries a fast-forward step;
+             * one without a run of hits ahead gets k = 0 and leaves at once.  Only every
+             * FF_PROBE-th iteration, so the round itself carries no detection work.  The
+             * lanes of a group are a field of the wave masks (8 bits for 8 nodes, 4 for 4);
+             * a field's top bit is set iff the field is non-zero, then spread over it. */
+            constexpr uint64_t FTOP = NP == 8 ? 0x8080808080808080ull : 0x8888888888888888ull;
+            constexpr uint64_t FLOW = ~FTOP;
+            const uint64_t busy = __ballot((nd.rh >> 8) != 0u) | ~liveb;
+            const uint64_t nzb = (((busy & FLOW) + FLOW) | busy) & FTOP;
+            const uint64_t one = (~nzb & FTOP) >> (NP - 1);
+            ffm |= (one << NP) - one;
         }
-        const uint64_t nlive = __ballot(live);
-        /* budget pass: once a slot of this wave found no new system, the wave's remaining
-         * systems get the late budget, so the launch's tail is not a system claimed last
-         * running its full budget at falling occupancy (the resume pass continues them) */
-        if (budget && late_rsh && (liveb & ~nlive)) rsh = late_rsh < rsh ? late_rsh : rsh;
-        liveb = nlive;
+        if (FF && ffm) round(std::true_type{});
+        else round(std::false_type{});
     }
 
     /* publish the workgroup's counters: its waves' rows summed in LDS, then one device-scope

@@ -116,6 +116,8 @@ def lib():
             "dsm_generate_text_device": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
+            if os.environ.get("DSM_LIB") and not hasattr(L, name):
+                continue        # an older A/B build without this entry point
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
         _lib = L

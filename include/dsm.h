@@ -148,8 +148,8 @@ typedef struct dsm_counters {
     uint64_t overflow_reruns;  /* systems re-run with the 256-deep inbox */
     uint64_t wave_rounds;      /* lock-step loop iterations summed over waves (cost model) */
     uint64_t resumed;          /* systems the two-pass schedule suspended and resumed      */
-    uint64_t ff_passes;        /* hit-run fast-forward passes (per wave, cost model)        */
-    uint64_t ff_steps;         /* their 8-instruction steps (per wave, cost model)          */
+    uint64_t ff_passes;        /* hit-run fast-forward steps of a system that advanced it   */
+    uint64_t ff_steps;         /* fast-forward steps per wave (cost model)                  */
     uint64_t reserved[2];
 } dsm_counters;
 

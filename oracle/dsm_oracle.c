@@ -302,6 +302,33 @@ static void issue(osys *y, int me, uint16_t ins) {
     }
 }
 
+/* test hook (tests/model/step_model.cpp): ONE action of node `me` of an np-node system whose
+ * node state is *s -- a message {type, sender, addr, value, bv, r2} handled (:177-566), or,
+ * with type < 0, the instruction `ins` issued (:590-687).  *s is updated; the staged sends
+ * go to out[k] = {dest, type, sender, addr, value, bv, r2}; returns 1 if an assert failed. */
+int orc_step(int np, int me, dsm_rec *s, int type, uint16_t ins, int sender, int addr, int value,
+             int bv, int r2, uint8_t (*out)[7], int *nout) {
+    osys y;
+    memset(&y, 0, sizeof y);
+    y.np = np; y.cap = DSM_REF_RING_CAP;
+    y.n[me].s = *s;
+    if (type < 0) {
+        issue(&y, me, ins);
+    } else {
+        omsg m = mk((uint8_t)type, sender, (uint8_t)addr);
+        m.value = (uint8_t)value; m.bv = (uint8_t)bv; m.r2 = (uint8_t)r2;
+        handle(&y, me, m);
+    }
+    *s = y.n[me].s;
+    for (int k = 0; k < y.nst; ++k) {
+        out[k][0] = y.st_dest[k]; out[k][1] = y.st_msg[k].type; out[k][2] = y.st_msg[k].sender;
+        out[k][3] = y.st_msg[k].addr; out[k][4] = y.st_msg[k].value; out[k][5] = y.st_msg[k].bv;
+        out[k][6] = y.st_msg[k].r2;
+    }
+    *nout = y.nst;
+    return y.assert_failed;
+}
+
 static void init_node(dsm_rec *s, int id) {                          /* :778-790, :144-145 */
     for (int i = 0; i < 16; ++i) {
         s->memory[i] = (uint8_t)(20 * id + i);

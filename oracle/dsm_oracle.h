@@ -50,6 +50,11 @@ void orc_set_round_limit(uint32_t limit);
 void orc_generate(int np, int dist, uint64_t seed, uint32_t n_instr, uint64_t first_sys,
                   uint64_t n_sys, uint16_t *traces, uint32_t *counts);
 
+/* One action of one node (test hook for the per-transition model, tests/model/): a message
+ * handled, or with type < 0 the instruction `ins` issued; *s updated, staged sends in out. */
+int orc_step(int np, int me, dsm_rec *s, int type, uint16_t ins, int sender, int addr, int value,
+             int bv, int r2, uint8_t (*out)[7], int *nout);
+
 /* printProcessorState text (assignment.c:824-876) of one record; returns length or -1. */
 int orc_format_dump(int node, const dsm_rec *r, char *buf, int cap);
 

@@ -125,7 +125,7 @@ def test_round_limit_message_bound(dsm, orc, limit_log2):
     assert cnt["status_ROUND_LIMIT"] == int(((ores["status"] & 0xFF) == 4).sum()) > 0
 
 
-@pytest.mark.parametrize("cap,ring", [(3, 12), (6, 4), (8, 8)])
+@pytest.mark.parametrize("cap,ring", [(3, 12), (6, 4), (5, 8)])
 def test_ring_overflow_beyond_inbox_limit(dsm, orc, cap, ring):
     """Inbox limit below the fast ring (reported by the fast kernel's hand-off + 256-deep
     re-run) and above it (the re-run sees the deeper inbox first)."""

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # tools/build_variant.sh <name> <sed-expr> [<sed-expr> ...] -- build libdsm.so from the
-# working tree with sed edits applied to csrc/dsm_engine.hip into abtmp/libdsm_<name>.so
+# working tree with sed edits applied to csrc/dsm_engine.hip into ab/libdsm_<name>.so
 # (kernel-variant A/B with tools/ab_lib.sh; the edits never touch the tree)
 set -e
 NAME=$1; shift
@@ -10,7 +10,7 @@ for e in "$@"; do sed -i "$e" "$T/csrc/dsm_engine.hip"; done
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$T/include"
 $H -c "$T/csrc/dsm_engine.hip" -o "$T/e.o" 2>"$T/warn.txt" || { cat "$T/warn.txt"; exit 1; }
 grep -i "spill\|occupancy" "$T/warn.txt" | head -5 || true
-mkdir -p abtmp
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$T/e.o" hp-assignment-2_amd/build/dsm_text.o hp-assignment-2_amd/build/dsm_host.o -o "abtmp/libdsm_$NAME.so"
+mkdir -p ab
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$T/e.o" hp-assignment-2_amd/build/dsm_text.o hp-assignment-2_amd/build/dsm_host.o -o "ab/libdsm_$NAME.so"
 rm -rf "$T"
-echo "abtmp/libdsm_$NAME.so"
+echo "ab/libdsm_$NAME.so"
