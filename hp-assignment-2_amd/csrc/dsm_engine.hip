@@ -316,7 +316,10 @@ sim_kernel(const SimArgs *Ap) {
      * (not with the issue-order trace or the seeded stalls of schedule exploration) */
     constexpr bool FF = (MODE & (M_TR | M_SX)) == 0;
     constexpr int SW = susp_words(RING);
-    constexpr uint32_t FF_PROBE = 16;   /* fast-forward probe every 16 iterations */
+    /* fast-forward probe interval: FF_PROBE iterations after a probe that found a group,
+     * doubling up to FF_PROBE_MAX after each one that found none (workloads without hit
+     * runs stop paying for the probe) */
+    constexpr uint32_t FF_PROBE = 16, FF_PROBE_MAX = 512;
 
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
     __shared__ uint32_t s_line[WAVES][4][64];        /* cache lines: addr | value << 8 | state << 16 */
@@ -343,7 +346,6 @@ sim_kernel(const SimArgs *Ap) {
     const int gdist = GEN ? Ap->dist : 0;
     const uint32_t stride = GEN ? 0u : Ap->stride;   /* >= 8, multiple of 8 (dsm_open) */
     const uint32_t lim_rsh = Ap->lim_rsh;                /* round limit 1 << lim_rsh       */
-    const uint32_t lim = 1u << lim_rsh;
     /* an inbox beyond ocap ends the round's system: the fast kernel hands it to the 256-deep
      * re-run (its ring holds RING), which reports RING_OVERFLOW beyond the inbox limit */
     const uint32_t ocap = FB || Ap->icap < (uint32_t)RING ? Ap->icap : (uint32_t)RING;
@@ -355,11 +357,14 @@ sim_kernel(const SimArgs *Ap) {
      * resident count of suspended systems (no host round trip): it uses the fewest slots
      * that hold an equal whole number of them, so the slots (all running systems of similar
      * remaining length) finish together; the other slots exit at once. */
-    uint64_t pool = (uint64_t)gridDim.x * WAVES * GPW;
-    if (resume && n) {
-        const uint64_t per = (n + pool - 1) / pool;
-        pool = (n + per - 1) / per;
-    }
+    auto pool_of = [&]() -> uint64_t {     /* recomputed where used (scalar registers are scarce) */
+        uint64_t pool = (uint64_t)gridDim.x * WAVES * GPW;
+        if (resume && n) {
+            const uint64_t per = (n + pool - 1) / pool;
+            pool = (n + per - 1) / per;
+        }
+        return pool;
+    };
 
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
@@ -429,7 +434,7 @@ sim_kernel(const SimArgs *Ap) {
         }
     };
 
-    if (G < n && G < pool) {
+    if (G < n && G < pool_of()) {
         live = true;
         start(G);
     } else {
@@ -437,7 +442,6 @@ sim_kernel(const SimArgs *Ap) {
     }
 
     uint32_t wrounds = 0;    /* loop iterations of this wave (uniform) */
-    uint32_t ffpass = 0, ffiter = 0;   /* fast-forward entries (groups) / steps (wave)      */
     uint64_t ffm = 0;                  /* lanes in fast-forward mode (wave-uniform)          */
     uint64_t liveb = __ballot(live);
     /* one lock-step round of every system of the wave; compiled twice: with the
@@ -461,7 +465,7 @@ sim_kernel(const SimArgs *Ap) {
                  * (the one that breaks the run).  The shift register cur / nxt keeps its meaning,
                  * so the mode has no state but the wave's lane mask. */
                 const bool inff = __builtin_amdgcn_inverse_ballot_w64(ffm);
-                ++ffiter;
+                if (lane == 0) s_cnt[wv][K_FFITER] += 1;     /* fast-forward steps of the wave */
                 uint32_t k = 8;
                 if (inff) {
                     const bool iss = (nd.ctl & C_WAIT) == 0u && nd.ip < nd.nins;
@@ -501,7 +505,7 @@ sim_kernel(const SimArgs *Ap) {
                     uint32_t r = iss ? (uint32_t)__builtin_ctz(~hm) : (dpend || !gany ? 0u : 8u);
                     if (iss && r > nd.nins - nd.ip) r = nd.nins - nd.ip;
                     /* the round limit: the round that reaches it runs normally */
-                    if (r > lim - 1u - rounds) r = lim - 1u - rounds;
+                    if (r > (1u << lim_rsh) - 1u - rounds) r = (1u << lim_rsh) - 1u - rounds;
                     k = gmin<NP>(r);
                     if (iss && k) {
                         uint32_t lval = 0, wm = 0;
@@ -537,7 +541,8 @@ sim_kernel(const SimArgs *Ap) {
                     }
                     rounds += k;
                 }
-                ffpass += (uint32_t)__builtin_popcountll(__ballot(inff && node == 0u && k != 0u));
+                const uint32_t adv = (uint32_t)__builtin_popcountll(__ballot(inff && node == 0u && k != 0u));
+                if (lane == 0) s_cnt[wv][K_FFPASS] += adv;   /* system steps that advanced */
                 ffm &= ~__ballot(inff && k < 8u);   /* those run this iteration's round normally */
             }
             /* still in the mode: no round here (the lane's bit of the wave-uniform mask) */
@@ -652,8 +657,7 @@ sim_kernel(const SimArgs *Ap) {
              * group's destination bytes */
             {
                 uint32_t m0 = o0 >> 24, m1 = o1 >> 24;
-                uint32_t b0 = 2 * node;            /* recomputed here, not kept in a register */
-                asm volatile("" : "+v"(b0));
+                const uint32_t b0 = 2 * node;
                 const uint32_t bit0 = 1u << b0, bit1 = 2u << b0;
                 if (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
                 if (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
@@ -721,8 +725,8 @@ sim_kernel(const SimArgs *Ap) {
             const bool gbad = ((badb >> gbase) & NPM) != 0;
             if (gact == 0) --rounds;
             /* budget pass: a system still running after 1 << rsh rounds is suspended */
-            const bool susp = budget && gact != 0 && !gbad && rounds >= (1u << rsh) && rounds < lim;
-            const bool done = live && (gact == 0 || gbad || rounds >= lim || susp);
+            const bool susp = budget && gact != 0 && !gbad && rounds >= (1u << rsh) && (rounds >> lim_rsh) == 0u;
+            const bool done = live && (gact == 0 || gbad || (rounds >> lim_rsh) != 0u || susp);
 
             const uint64_t doneb = __ballot(done);
             if (doneb) {
@@ -777,6 +781,7 @@ sim_kernel(const SimArgs *Ap) {
                             atomicMax(&s_cnt[wv][K_MAXR], (unsigned long long)rounds);
                         }
                         /* next system: static first assignment, then 8 sharded counters */
+                        const uint64_t pool = pool_of();
                         const uint64_t rs = n > pool ? (n - pool + 7) / 8 : 0;
                         while (tried < 8) {
                             const uint64_t lo = pool + (uint64_t)shard * rs;
@@ -820,28 +825,58 @@ sim_kernel(const SimArgs *Ap) {
             liveb = nlive;
     };
 
-    for (;;) {
-        if (liveb == 0) break;
-        ++wrounds;
-
-        /* FF: lanes of groups in fast-forward mode do one fast-forward step (0) this
-         * iteration instead of a normal round; when every live lane is in that mode the
-         * normal round is skipped altogether */
-        if (FF && (wrounds & (FF_PROBE - 1u)) == 0u) {
-            /* probe: every group whose inboxes are all empty tries a fast-forward step;
-             * one without a run of hits ahead gets k = 0 and leaves at once.  Only every
-             * FF_PROBE-th iteration, so the round itself carries no detection work.  The
-             * lanes of a group are a field of the wave masks (8 bits for 8 nodes, 4 for 4);
-             * a field's top bit is set iff the field is non-zero, then spread over it. */
-            constexpr uint64_t FTOP = NP == 8 ? 0x8080808080808080ull : 0x8888888888888888ull;
-            constexpr uint64_t FLOW = ~FTOP;
-            const uint64_t busy = __ballot((nd.rh >> 8) != 0u) | ~liveb;
-            const uint64_t nzb = (((busy & FLOW) + FLOW) | busy) & FTOP;
-            const uint64_t one = (~nzb & FTOP) >> (NP - 1);
-            ffm |= (one << NP) - one;
+    /* the wave alternates between two loops, each with its own copy of the round: the plain
+     * one (no fast-forward code at all) and, while some group is in fast-forward mode, the
+     * one with the fast-forward step (0).  Separate inner loops keep the plain loop's
+     * register allocation and code as if fast-forward did not exist. */
+    uint32_t pint = FF_PROBE, pcd = FF_PROBE;   /* probe interval / countdown (uniform) */
+    auto probe = [&]() {
+        /* a group enters fast-forward mode when its inboxes are all empty, no node is about
+         * to dump, and the next instruction of every issuing node (one at least) is a hit.
+         * Only every so many iterations, so the round itself carries no detection work.
+         * The lanes of a group are a field of the wave masks (8 bits for 8 nodes, 4 for 4);
+         * a field's top bit is set iff the field is non-zero, then spread over it. */
+        constexpr uint64_t FTOP = NP == 8 ? 0x8080808080808080ull : 0x8888888888888888ull;
+        constexpr uint64_t FLOW = ~FTOP;
+        const bool waits = (nd.ctl & C_WAIT) != 0u;
+        const bool iss = !waits && nd.ip < nd.nins;
+        bool hit = false;
+        if (iss) {
+            const uint32_t ins = GEN ? gen_instr<NP>(gmul, gdist, gfirst + sys, node, nd.ip)
+                                     : (cur[0] & 0xFFFFu);
+            const uint32_t a = (ins >> 8) & 0x7Fu;
+            const uint32_t lw = s_line[wv][a & 3u][lane];
+            const uint32_t ls = lw >> 16;
+            hit = (lw & 0xFFu) == a && ((ins & 0x8000u) ? ls <= DT_CE : ls != DT_CI);
         }
-        if (FF && ffm) round(std::true_type{});
-        else round(std::false_type{});
+        const bool block = (nd.rh >> 8) != 0u || (iss && !hit) ||
+                           (!waits && !iss && (nd.ctl & C_DUMPED) == 0u);
+        const uint64_t hitb = __ballot(hit);
+        const uint64_t nzh = (((hitb & FLOW) + FLOW) | hitb) & FTOP;
+        const uint64_t busy = __ballot(block) | ~liveb;
+        const uint64_t nzb = (((busy & FLOW) + FLOW) | busy) & FTOP;
+        const uint64_t one = (~nzb & nzh) >> (NP - 1);
+        ffm |= (one << NP) - one;
+        pint = one ? FF_PROBE : (pint < FF_PROBE_MAX ? 2u * pint : FF_PROBE_MAX);
+        pcd = pint;
+    };
+    for (;;) {
+        for (;;) {                                       /* plain rounds */
+            if (liveb == 0) break;
+            ++wrounds;
+            if (FF && --pcd == 0u) {
+                probe();
+                if (ffm) break;
+            }
+            round(std::false_type{});
+        }
+        if (!FF || liveb == 0) break;
+        for (;;) {                                       /* rounds with fast-forward */
+            round(std::true_type{});
+            if (ffm == 0 || liveb == 0) break;
+            ++wrounds;
+            if (--pcd == 0u) probe();
+        }
     }
 
     /* publish the workgroup's counters: its waves' rows summed in LDS, then one device-scope
@@ -849,8 +884,6 @@ sim_kernel(const SimArgs *Ap) {
      * depend on the order, so no separate reduction pass is needed) */
     if (lane == 0) {
         s_cnt[wv][K_WROUNDS] = wrounds;
-        s_cnt[wv][K_FFPASS] = ffpass;
-        s_cnt[wv][K_FFITER] = ffiter;
     }
     __syncthreads();
     if (threadIdx.x < K_N) {
