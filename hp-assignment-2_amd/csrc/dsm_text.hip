@@ -259,8 +259,11 @@ DEVI uint32_t lowmask(uint32_t n) { return n >= 32u ? 0xFFFFFFFFu : (1u << n) - 
 /* One file per wave; windows of 64 x BPL bytes, double-buffered in registers (the next
  * window's loads are in flight while this one is scanned), staged in LDS for the chunk
  * reads. */
+#ifndef PARSE_OCC
+#define PARSE_OCC 6
+#endif
 template <uint32_t BPL>
-__global__ void __launch_bounds__(64 * PW) parse_kernel(const uint8_t *text, const uint64_t *off,
+__global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PARSE_OCC))) parse_kernel(const uint8_t *text, const uint64_t *off,
                                                       uint64_t n_files, uint32_t cap,
                                                       uint32_t stride, int np, uint16_t *traces,
                                                       uint32_t *counts, int32_t *status) {
