@@ -427,7 +427,8 @@ def main():
             "instructions_per_s": round(c["instrs"] * K / elapsed_max, 1),
             "counters": {k: c[k] for k in ("msgs", "instrs", "rounds", "systems", "max_rounds",
                                            "overflow_reruns", "wave_rounds", "resumed",
-                                           "ff_passes", "ff_steps", "status_COMPLETED",
+                                           "ff_passes", "ff_steps", "ff_sample_instrs",
+                                           "ff_sample_runs", "status_COMPLETED",
                                            "status_DEADLOCKED")},
             "kernel_ms": [round(x, 3) for x in kms],
             "sum_final_hash": hex(c["sum_final_hash"]),

@@ -71,6 +71,9 @@ struct SimArgs {
     uint32_t rsh;                   /* round-limit test: rounds >> rsh != 0                  */
     uint32_t budget;                /* budget pass: suspend at 1 << rsh rounds               */
     uint32_t resume;                /* resume pass: start() restores a suspended system      */
+    uint32_t ffsel;                 /* one of a fast-forward / plain pair of launches: run only
+                                     * if scan's verdict picks this kernel (ffscan_kernel)    */
+    const uint32_t *scan;           /* [sampled instructions, 8-hit-run ends] (ffscan_kernel) */
     uint32_t late_rsh;              /* budget pass: the budget once a wave finds no new work  */
     uint32_t *susp;                 /* [sys][word][node] suspended state (susp_words)        */
     uint32_t *susp_list;            /* budget pass: suspended system ids                     */
@@ -104,7 +107,7 @@ constexpr uint32_t C_WAIT = DT_CTL_WAIT, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C
 /* counter slots (dsm_counters order) */
 enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
        K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_RESUMED = 27,
-       K_FFPASS = 28, K_FFITER = 29, K_N = 32 };
+       K_FFPASS = 28, K_FFITER = 29, K_SCANI = 30, K_SCANR = 31, K_N = 32 };
 constexpr uint32_t RSH_MAX = 22;    /* 1 << 22 == DSM_MAX_ROUNDS */
 static_assert((1u << RSH_MAX) == DSM_MAX_ROUNDS, "DSM_MAX_ROUNDS");
 /* suspended node state: memory/bitVector (8), lines (4), ring (RING), dst, ctl, ip, nins, rh,
@@ -300,9 +303,68 @@ enum : int {
     M_TC = 1,   /* per-type message counters (DSM_F_TYPE_COUNTS): 16-bit fields per node and
                  * system, added to the wave counters when the system finishes             */
     M_TR = 2,   /* issue-order trace (DSM_F_ISSUE_TRACE): DEBUG_INSTR order, :595-598      */
-    M_SX = 4    /* seeded schedule exploration (dsm_set_schedule): a node with an action
+    M_SX = 4,   /* seeded schedule exploration (dsm_set_schedule): a node with an action
                  * may stall for the round (oracle/dsm_common.h dsm_sched_act)            */
+    M_LIM = 8,  /* run-time round limit / inbox limit (dsm_set_round_limit,
+                 * dsm_set_inbox_limit) for the bench mode, which otherwise has them as
+                 * constants (measured: the two limits as SGPRs cost 1.5-2% in the round)  */
+    M_NOFF = 16 /* the bench mode without the hit-run fast-forward (ffscan_kernel picks)     */
 };
+
+/* ---- fast-forward verdict --------------------------------------------------------------
+ * The hit-run fast-forward (sim_kernel step (0)) pays only where nodes issue long runs of
+ * hits; elsewhere its second copy of the round costs the plain round ~3% (C3).  Before the
+ * packed path's budget pass, ffscan_kernel replays the first instructions of a sample of
+ * node traces through a private 4-line tag model (each line holds the last address that
+ * mapped to it, assignment.c:177-184 indexing; no coherence) and counts the instructions
+ * that end a run of 8 hits.  Both kernels of the pair are launched; the one this verdict
+ * does not pick exits at once.  The choice only moves time: both produce the same results
+ * (tests/test_gpu_fastforward.py). */
+constexpr uint32_t SCAN_SYS = 4096, SCAN_INSTR = 256;
+DEVI bool ff_verdict(const uint32_t *scan) {
+    const uint32_t tot = scan[0], run8 = scan[1];
+    return run8 != 0u && (uint64_t)run8 * 16u >= tot;    /* >= 1/16 of the sample */
+}
+template <int NP>
+__global__ void __launch_bounds__(256) ffscan_kernel(const uint16_t *traces, const uint32_t *counts,
+                                                     uint32_t stride, uint64_t n_sys, uint32_t *scan,
+                                                     unsigned long long *counters) {
+    const uint32_t S = n_sys < SCAN_SYS ? (uint32_t)n_sys : SCAN_SYS;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    uint32_t tot = 0, run8 = 0;
+    if (t < S * NP) {
+        const uint64_t sys = (uint64_t)(t / NP) * n_sys / S;
+        const uint32_t node = t % NP;
+        const uint32_t c = counts[sys * NP + node];
+        const uint32_t n = (c < stride ? c : stride) < SCAN_INSTR ? (c < stride ? c : stride) : SCAN_INSTR;
+        const uint16_t *tp = traces + (sys * NP + node) * (uint64_t)stride;
+        uint32_t tags = 0xFFFFFFFFu, run = 0;
+        for (uint32_t i = 0; i < n; i += 8) {
+            const uint4 v = ld16(tp + i);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (i + j < n) {
+                    const uint32_t a = (w[j >> 1] >> (16 * (j & 1) + 8)) & 0x7Fu, sh = (a & 3u) * 8u;
+                    run = ((tags >> sh) & 0xFFu) == a ? run + 1u : 0u;
+                    tags = (tags & ~(0xFFu << sh)) | (a << sh);
+                    run8 += run >= 8u ? 1u : 0u;
+                }
+            }
+        }
+        tot = n;
+    }
+    for (int o = 1; o < 64; o <<= 1) {
+        tot += __shfl_xor(tot, o, 64);
+        run8 += __shfl_xor(run8, o, 64);
+    }
+    if ((threadIdx.x & 63u) == 0 && tot) {
+        atomicAdd(&scan[0], tot);
+        atomicAdd(&scan[1], run8);
+        atomicAdd(&counters[K_SCANI], (unsigned long long)tot);
+        atomicAdd(&counters[K_SCANR], (unsigned long long)run8);
+    }
+}
 
 template <int NP, int RING, int WAVES, bool GEN, int MODE, int OCC = 5>
 __global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
@@ -311,15 +373,20 @@ sim_kernel(const SimArgs *Ap) {
     constexpr uint32_t NPM = (1u << NP) - 1u;
     constexpr bool FB = (RING == FB_RING);   /* the 256-deep re-run kernel                */
     constexpr bool TC = (MODE & M_TC) != 0, TR = (MODE & M_TR) != 0, SX = (MODE & M_SX) != 0;
-    constexpr bool BUD = MODE == 0 && !FB && !GEN;   /* the two-pass schedule's suspend/resume */
+    constexpr bool BUD = (MODE & ~(M_LIM | M_NOFF)) == 0 && !FB && !GEN;   /* two-pass schedule */
+    constexpr bool LIM = FB || (MODE & ~M_NOFF) != 0;   /* limits read at run time, else constants */
     /* hit-run fast-forward: wherever the order of issues inside a round is not observed
      * (not with the issue-order trace or the seeded stalls of schedule exploration) */
-    constexpr bool FF = (MODE & (M_TR | M_SX)) == 0;
+    constexpr bool FF = (MODE & (M_TR | M_SX | M_NOFF)) == 0;
     constexpr int SW = susp_words(RING);
     /* fast-forward probe interval: FF_PROBE iterations after a probe that found a group,
      * doubling up to FF_PROBE_MAX after each one that found none (workloads without hit
      * runs stop paying for the probe) */
     constexpr uint32_t FF_PROBE = 16, FF_PROBE_MAX = 512;
+
+    /* a fast-forward / plain pair: the kernel the trace scan did not pick exits at once
+     * (wave-uniform scalar loads; the whole workgroup returns before any barrier) */
+    if (!FB && Ap->ffsel && ff_verdict(Ap->scan) != FF) return;
 
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
     __shared__ uint32_t s_line[WAVES][4][64];        /* cache lines: addr | value << 8 | state << 16 */
@@ -345,10 +412,10 @@ sim_kernel(const SimArgs *Ap) {
     const uint64_t gfirst = GEN ? Ap->first_sys : 0;
     const int gdist = GEN ? Ap->dist : 0;
     const uint32_t stride = GEN ? 0u : Ap->stride;   /* >= 8, multiple of 8 (dsm_open) */
-    const uint32_t lim_rsh = Ap->lim_rsh;                /* round limit 1 << lim_rsh       */
+    const uint32_t lim_rsh = LIM ? Ap->lim_rsh : RSH_MAX;   /* round limit 1 << lim_rsh    */
     /* an inbox beyond ocap ends the round's system: the fast kernel hands it to the 256-deep
      * re-run (its ring holds RING), which reports RING_OVERFLOW beyond the inbox limit */
-    const uint32_t ocap = FB || Ap->icap < (uint32_t)RING ? Ap->icap : (uint32_t)RING;
+    const uint32_t ocap = FB || (LIM && Ap->icap < (uint32_t)RING) ? Ap->icap : (uint32_t)RING;
     uint32_t rsh = BUD && Ap->rsh < lim_rsh ? Ap->rsh : lim_rsh;   /* wave-uniform (an SGPR) */
     const uint32_t late_rsh = BUD ? Ap->late_rsh : 0u;
     const bool budget = BUD && Ap->budget != 0, resume = BUD && Ap->resume != 0;
@@ -369,10 +436,11 @@ sim_kernel(const SimArgs *Ap) {
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
     uint64_t sys = 0;
-    /* this node's trace slot, recomputed where used (a per-lane 64-bit pointer kept across
-     * the round loop would push the kernel over its VGPR budget) */
+    /* this node's trace slot, set when a system starts (measured: recomputing it at each
+     * refill costs more than the two VGPRs) */
     const uint16_t *const traces = Ap->traces;
     auto tslot = [&]() { return traces + (sys * NP + node) * (uint64_t)stride; };
+    const uint16_t *tb = nullptr;
     uint32_t rounds = 0, rmsg = 0;
     bool live = false;
     uint32_t tc[7] = {0, 0, 0, 0, 0, 0, 0};                                  /* TC only */
@@ -399,6 +467,7 @@ sim_kernel(const SimArgs *Ap) {
             nd.rh = q[4 * NP]; nd.nmsg = q[5 * NP]; rounds = q[6 * NP];
 #pragma unroll
             for (int k = 0; k < 4; ++k) { cur[k] = q[(7 + k) * NP]; nxt[k] = q[(11 + k) * NP]; }
+            if (!GEN) tb = tslot();
             rmsg = s_ring[wv][nd.rh & 0xFFu][lane];          /* the head, as the loop keeps it */
             return;
         }
@@ -424,7 +493,7 @@ sim_kernel(const SimArgs *Ap) {
         } else {
             const uint32_t c = Ap->counts[sys * NP + node];
             nd.nins = c < stride ? c : stride;
-            const uint16_t *tb = tslot();
+            tb = tslot();
             /* both chunks unconditionally (in-slot), then drain them here, once per system:
              * the round loop's only vmcnt wait is then the refill rotation */
             const uint4 v0 = ld16(tb), v1 = ld16(tb + (stride > 8 ? 8 : 0));
@@ -533,7 +602,7 @@ sim_kernel(const SimArgs *Ap) {
                             ff_shift(X, cross ? k - m : k, cur);
                             if (cross) {   /* the chunk after: used next iteration at the earliest */
                                 const uint32_t pc = ((nd.ip >> 3) + 2) * 8u;
-                                const uint4 v = ld16(tslot() + (pc + 8u <= stride ? pc : stride - 8u));
+                                const uint4 v = ld16(tb + (pc + 8u <= stride ? pc : stride - 8u));
                                 nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
                             }
                         }
@@ -577,7 +646,7 @@ sim_kernel(const SimArgs *Ap) {
              * same basic block stalls the whole wave on HBM). */
             const bool refill = !GEN && doIssue && ((nd.ip + 1) & 7u) == 0 && nd.ip + 1 < nd.nins;
             uint4 pf;
-            if (refill) pf = ld16(tslot() + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
+            if (refill) pf = ld16(tb + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
             const uint32_t headn = (head0 + 1 == (uint32_t)RING) ? 0u : head0 + 1;
             nd.rh = hasMsg ? (headn | ((cnt0 - 1) << 8)) : nd.rh;
             uint32_t w = rmsg;
@@ -1016,8 +1085,8 @@ sim_fn fast_mode(int ring) {
      * the overflow-prone depth 4 (which exercises the 256-deep re-run) for the others */
     switch (ring) {
     case 4: return sim_kernel<NP, 4, FW, GEN, MODE>;
-    case 8: if (MODE == 0) return sim_kernel<NP, 8, FW, GEN, 0>; break;
-    case 16: if (MODE == 0) return sim_kernel<NP, 16, FW, GEN, 0>; break;
+    case 8: if ((MODE & ~M_NOFF) == 0) return sim_kernel<NP, 8, FW, GEN, MODE & M_NOFF>; break;
+    case 16: if ((MODE & ~M_NOFF) == 0) return sim_kernel<NP, 16, FW, GEN, MODE & M_NOFF>; break;
     default: break;
     }
     return sim_kernel<NP, 12, FW, GEN, MODE>;
@@ -1032,6 +1101,10 @@ sim_fn fast_np_gen(int ring, int mode) {
     case 5: return fast_mode<NP, GEN, 5>(ring);
     case 6: return fast_mode<NP, GEN, 6>(ring);
     case 7: return fast_mode<NP, GEN, 7>(ring);
+    case M_LIM: return fast_mode<NP, GEN, M_LIM>(ring);
+    case M_NOFF:                        /* packed path only (ffscan_kernel reads traces) */
+        if constexpr (!GEN) return fast_mode<NP, GEN, M_NOFF>(ring);
+        break;
     default: return fast_mode<NP, GEN, 0>(ring);
     }
 }
@@ -1041,7 +1114,7 @@ sim_fn pick_fast(int np, int ring, bool gen, int mode) {
 }
 template <int NP, bool GEN>
 sim_fn fb_np_gen(int mode) {
-    switch (mode) {
+    switch (mode & 7) {       /* the re-run always reads the limits (LIM) */
     case 1: return sim_kernel<NP, FB_RING, 1, GEN, 1, 1>;
     case 2: return sim_kernel<NP, FB_RING, 1, GEN, 2, 1>;
     case 3: return sim_kernel<NP, FB_RING, 1, GEN, 3, 1>;
@@ -1083,6 +1156,7 @@ static_assert(sizeof(SimArgsPack) % 4 == 0, "SimArgsPack words");
 #define CTRL_OVF 512
 #define CTRL_RES 1024       /* claim shards of the resume pass */
 #define CTRL_SUSP 1536      /* systems the budget pass suspended */
+#define CTRL_SCAN 1792      /* ffscan_kernel's sample counts */
 
 /* Two-pass schedule (bench mode: MODE 0, packed traces).  A system's length is unknown until
  * it ends, and ~14% of C3 systems run ~12.5k rounds against a median of ~650: in one
@@ -1136,6 +1210,7 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->late_log2 = env_u32("DSM_LATE_LOG2", 10);
     c->round_limit_log2 = RSH_MAX;
     c->inbox_limit = FB_RING;
+    c->ff_mode = DSM_FF_AUTO;
     c->fmt_tile = (int)env_u32("DSM_FMT", 132);
     c->parse_bpl = (int)env_u32("DSM_PARSE_BPL", 32);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -1201,6 +1276,12 @@ extern "C" int dsm_set_round_limit(dsm_ctx *c, uint32_t limit_log2) {
     return DSM_OK;
 }
 
+extern "C" int dsm_set_fast_forward(dsm_ctx *c, int mode) {
+    if (!c || mode < DSM_FF_OFF || mode > DSM_FF_AUTO) return DSM_E_INVAL;
+    c->ff_mode = mode;
+    return DSM_OK;
+}
+
 extern "C" int dsm_set_inbox_limit(dsm_ctx *c, uint32_t cap) {
     if (!c || cap > (uint32_t)FB_RING) return DSM_E_INVAL;
     c->inbox_limit = cap ? cap : (uint32_t)FB_RING;
@@ -1217,9 +1298,16 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     HIPCK(hipSetDevice(c->device));
     const int np = c->cfg.np, gpw = 64 / np;
     const bool tr = (c->cfg.flags & DSM_F_ISSUE_TRACE) != 0;
-    const int mode = ((c->cfg.flags & DSM_F_TYPE_COUNTS) ? M_TC : 0) | (tr ? M_TR : 0) |
-                     (c->sched_thresh < DSM_SCHED_LOCKSTEP ? M_SX : 0);
-    const sim_fn fast = pick_fast(np, c->ring, gen, mode), fb = pick_fallback(np, gen, mode);
+    int mode = ((c->cfg.flags & DSM_F_TYPE_COUNTS) ? M_TC : 0) | (tr ? M_TR : 0) |
+               (c->sched_thresh < DSM_SCHED_LOCKSTEP ? M_SX : 0);
+    /* the bench mode with a round limit or an inbox limit below the fast ring */
+    if (mode == 0 && (c->round_limit_log2 != RSH_MAX || c->inbox_limit < (uint32_t)c->ring)) mode = M_LIM;
+    /* the bench mode on the packed path: the hit-run fast-forward per dsm_set_fast_forward;
+     * in auto, a pair of launches per pass, picked on the device by ffscan_kernel */
+    const bool plain_only = mode == 0 && !gen && c->ff_mode == DSM_FF_OFF;
+    const bool pair = mode == 0 && !gen && c->ff_mode == DSM_FF_AUTO;
+    const sim_fn fast = pick_fast(np, c->ring, gen, plain_only ? M_NOFF : mode), fb = pick_fallback(np, gen, mode);
+    const sim_fn fast_nf = pair ? pick_fast(np, c->ring, gen, M_NOFF) : nullptr;
     int nb_fast = 0, nb_fb = 0;
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fast, (const void *)fast, 64 * FW, 0));
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fb, (const void *)fb, 64, 0));
@@ -1232,7 +1320,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     uint64_t dblocks = (n_sys * np + 255) / 256;
     if (dblocks > (uint64_t)c->cus * 8) dblocks = (uint64_t)c->cus * 8;
     /* two-pass schedule on the packed path in bench mode */
-    const uint32_t blog = (mode == 0 && !gen) ? c->budget_log2 : 0u;
+    const uint32_t blog = ((mode & ~M_LIM) == 0 && !gen) ? c->budget_log2 : 0u;
     int rc;
     if ((rc = ensure(&c->d_ovf_list, &c->ovf_cap, (size_t)n_sys))) return rc;
     const int ring_eff = (mode && c->ring != 4) ? 12 : c->ring;   /* fast_mode's choice */
@@ -1308,18 +1396,36 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     C.budget = 0;
     C.late_rsh = 0;
     C.resume = 1;
+    A.scan = C.scan = c->d_ctrl + CTRL_SCAN;
+    A.ffsel = C.ffsel = pair ? 1u : 0u;
     hipLaunchKernelGGL(args_kernel, dim3(1), dim3(64), 0, st, pk, c->d_args);
     HIPCK(hipGetLastError());
 
     const bool timed = (c->cfg.flags & DSM_F_TIMING) != 0;
     const int slot = (int)(c->runs_timed % DSM_TIMING_RING);
     if (timed) HIPCK(hipEventRecord(c->tev0[slot], st));
-    hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, (const SimArgs *)c->d_args);
-    HIPCK(hipGetLastError());
-    /* resume pass at the budget pass's grid: it sizes itself from the suspended count */
-    if (blog) {
-        hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, (const SimArgs *)(c->d_args + 2));
+    if (pair) {
+        const uint32_t S = n_sys < SCAN_SYS ? (uint32_t)n_sys : SCAN_SYS;
+        const unsigned sb = (unsigned)((S * (uint32_t)np + 255u) / 256u);
+        if (np == 4)
+            hipLaunchKernelGGL(ffscan_kernel<4>, dim3(sb), dim3(256), 0, st, d_traces, d_counts,
+                               (uint32_t)c->cfg.max_instr, n_sys, c->d_ctrl + CTRL_SCAN,
+                               reinterpret_cast<unsigned long long *>(d_counters));
+        else
+            hipLaunchKernelGGL(ffscan_kernel<8>, dim3(sb), dim3(256), 0, st, d_traces, d_counts,
+                               (uint32_t)c->cfg.max_instr, n_sys, c->d_ctrl + CTRL_SCAN,
+                               reinterpret_cast<unsigned long long *>(d_counters));
         HIPCK(hipGetLastError());
+    }
+    for (int pass = 0; pass < (blog ? 2 : 1); ++pass) {
+        /* resume pass at the budget pass's grid: it sizes itself from the suspended count */
+        const SimArgs *a = (const SimArgs *)(c->d_args + 2 * pass);
+        hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, a);
+        HIPCK(hipGetLastError());
+        if (pair) {
+            hipLaunchKernelGGL(fast_nf, dim3(grid_fast), dim3(64 * FW), 0, st, a);
+            HIPCK(hipGetLastError());
+        }
     }
     if (timed) {
         HIPCK(hipEventRecord(c->tev1[slot], st));

@@ -47,6 +47,7 @@ struct dsm_ctx {
     /* two-pass schedule and round limit (dsm_set_budget / dsm_set_round_limit; defaults from
      * DSM_BUDGET_LOG2 / DSM_LATE_LOG2, read once at dsm_open) */
     uint32_t budget_log2, late_log2, round_limit_log2, inbox_limit;
+    int ff_mode;                       /* DSM_FF_OFF / ON / AUTO */
     /* dsm_text.hip tuning (DSM_FMT / DSM_PARSE_BPL, read once at dsm_open) */
     int fmt_tile, parse_bpl;
     uint64_t sched_seed;             /* dsm_set_schedule                                     */

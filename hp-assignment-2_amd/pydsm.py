@@ -19,6 +19,7 @@ TYPE_NAMES = ["READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID
               "EVICT_SHARED", "EVICT_MODIFIED"]
 STATUS_NAMES = ["COMPLETED", "DEADLOCKED", "RING_OVERFLOW", "ASSERT_FAILED", "ROUND_LIMIT"]
 DIST = {"uniform": 0, "hot": 1, "evict": 2}
+FF_OFF, FF_ON, FF_AUTO = 0, 1, 2             # dsm_set_fast_forward
 F_SNAPSHOTS = 1
 F_TIMING = 2
 F_TYPE_COUNTS = 4
@@ -31,8 +32,8 @@ COUNTER_FIELDS = ([f"msgs_{t}" for t in TYPE_NAMES] +
                   ["msgs", "instrs", "rounds", "systems"] +
                   [f"status_{s}" for s in STATUS_NAMES] +
                   ["sum_dump_hash", "sum_final_hash", "max_rounds", "overflow_reruns",
-                   "wave_rounds", "resumed", "ff_passes", "ff_steps"] +
-                  [f"reserved{i}" for i in range(2)])
+                   "wave_rounds", "resumed", "ff_passes", "ff_steps", "ff_sample_instrs",
+                   "ff_sample_runs"])
 assert len(COUNTER_FIELDS) == 32
 
 DUMP_BASE, DUMP_MAX, DUMP_SLOT = 1954, 1958, 1968
@@ -100,6 +101,7 @@ def lib():
             "dsm_set_budget": (i32, [vp, u32, u32]),
             "dsm_set_round_limit": (i32, [vp, u32]),
             "dsm_set_inbox_limit": (i32, [vp, u32]),
+            "dsm_set_fast_forward": (i32, [vp, i32]),
             "dsm_parse_trace_file": (i32, [ctypes.c_char_p, vp, u32, ctypes.POINTER(u32)]),
             "dsm_load_test_dir": (i32, [ctypes.c_char_p, i32, u32, vp, u32, vp]),
             "dsm_format_dump": (i32, [i32, vp, ctypes.c_char_p, ctypes.c_size_t]),
@@ -312,6 +314,10 @@ class Engine:
 
     def set_inbox_limit(self, cap):
         _check(lib().dsm_set_inbox_limit(self.ctx, cap), "dsm_set_inbox_limit")
+
+    def set_fast_forward(self, mode):
+        """FF_OFF / FF_ON / FF_AUTO (dsm_set_fast_forward): only time depends on it."""
+        _check(lib().dsm_set_fast_forward(self.ctx, mode), "dsm_set_fast_forward")
 
     def launch_info(self):
         li = LaunchInfo()

@@ -150,7 +150,8 @@ typedef struct dsm_counters {
     uint64_t resumed;          /* systems the two-pass schedule suspended and resumed      */
     uint64_t ff_passes;        /* hit-run fast-forward steps of a system that advanced it   */
     uint64_t ff_steps;         /* fast-forward steps per wave (cost model)                  */
-    uint64_t reserved[2];
+    uint64_t ff_sample_instrs; /* DSM_FF_AUTO: instructions of the sampled traces           */
+    uint64_t ff_sample_runs;   /* ... of them ending a run of 8 hits (a private 4-line model) */
 } dsm_counters;
 
 typedef struct dsm_ctx dsm_ctx;
@@ -253,6 +254,15 @@ int dsm_set_round_limit(dsm_ctx *ctx, uint32_t limit_log2);
 /* Inbox limit of the following runs (MSG_BUFFER_SIZE, assignment.c:12; 1..256, 0 = 256): an
  * append beyond it ends the system with DSM_RING_OVERFLOW (the reference spins, :715-724). */
 int dsm_set_inbox_limit(dsm_ctx *ctx, uint32_t cap);
+/* Hit-run fast-forward of the following packed-path runs in the bench mode (no type counts,
+ * issue trace or schedule exploration): DSM_FF_AUTO (default) samples the traces on the
+ * device first and runs the fast-forward kernel only where nodes issue long runs of hits;
+ * DSM_FF_ON / DSM_FF_OFF force it.  Results never depend on it (only time does); the
+ * sample's counts are reported in dsm_counters.ff_sample_*. */
+#define DSM_FF_OFF 0
+#define DSM_FF_ON 1
+#define DSM_FF_AUTO 2
+int dsm_set_fast_forward(dsm_ctx *ctx, int mode);
 
 /* ---- initializeProcessor's trace reader on the GPU (:802-818) ---------------------- *
  * n_files core files concatenated in d_text; file f is d_text[d_offsets[f] .. d_offsets[f+1])

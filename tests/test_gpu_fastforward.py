@@ -125,3 +125,28 @@ def test_round_limit_matches_reference_text(dsm, orc):
         eng.set_round_limit(9)
         res, _ = eng.run_generated("hot", 3, 4096, 0, n)
     _cmp(res, ref)
+
+
+@pytest.mark.parametrize("dist", ["uniform", "hot", "evict"])
+def test_fast_forward_modes_agree(dsm, orc, dist):
+    """dsm_set_fast_forward: off, on and auto give the oracle's results; auto's device-side
+    trace sample picks the fast-forward kernel on the hot-line workload only (its counters
+    show which kernel of the pair ran)."""
+    n = 4096
+    tr, cn = orc.generate(8, dist, 21, 4096, 0, n)
+    ores, _ = orc.run_packed(8, tr, cn, nthreads=16)[:2]
+    out = {}
+    with dsm.Engine(8, 4096) as eng:
+        for m in (dsm.FF_OFF, dsm.FF_ON, dsm.FF_AUTO):
+            eng.set_fast_forward(m)
+            out[m] = eng.run_packed(tr, cn)
+            _cmp(out[m][0], ores)
+    off, on, auto = out[dsm.FF_OFF][1], out[dsm.FF_ON][1], out[dsm.FF_AUTO][1]
+    assert off["ff_passes"] == 0 and off["ff_steps"] == 0 and off["ff_sample_instrs"] == 0
+    assert on["ff_sample_instrs"] == 0
+    assert auto["ff_sample_instrs"] == min(n, 4096) * 8 * 256
+    picked = auto["ff_sample_runs"] * 16 >= auto["ff_sample_instrs"] and auto["ff_sample_runs"] > 0
+    assert picked == (dist == "hot")
+    assert (auto["ff_steps"] > 0) == picked
+    if dist == "hot":
+        assert on["ff_passes"] > 0 and auto["ff_passes"] > 0
