@@ -369,9 +369,14 @@ def main():
         # resume pass, run_engine's two-pass schedule): bytes and time are per step, i.e. the
         # sum over both launches (rocprof lists 2 sim_kernel dispatches per step)
         launches = 2 if li.get("resume_blocks") else 1
+        # which kernel of the fast-forward / plain pair ran (dsm_set_fast_forward AUTO)
+        ff_picked = (local_c["ff_sample_runs"] > 0 and
+                     16 * local_c["ff_sample_runs"] >= local_c["ff_sample_instrs"]) or args.fused
         roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
-                    kernel="sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel; 4-wave groups, ring 12, packed traces)"
+                    kernel=("sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel with the hit-run fast-forward"
+                            if ff_picked else "sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain")
+                           + "; 4-wave groups, ring 12, packed traces; picked per run by ffscan_kernel's trace sample)"
                            + (f"; budget pass (2^{li['budget_log2']} rounds) + resume pass" if launches == 2 else ""),
                     launches_per_step=launches,
                     algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),

@@ -382,7 +382,7 @@ sim_kernel(const SimArgs *Ap) {
     /* fast-forward probe interval: FF_PROBE iterations after a probe that found a group,
      * doubling up to FF_PROBE_MAX after each one that found none (workloads without hit
      * runs stop paying for the probe) */
-    constexpr uint32_t FF_PROBE = 16, FF_PROBE_MAX = 512;
+    constexpr uint32_t FF_PROBE = 4, FF_PROBE_MAX = 512;
 
     /* a fast-forward / plain pair: the kernel the trace scan did not pick exits at once
      * (wave-uniform scalar loads; the whole workgroup returns before any barrier) */
@@ -539,15 +539,14 @@ sim_kernel(const SimArgs *Ap) {
                 if (inff) {
                     const bool iss = (nd.ctl & C_WAIT) == 0u && nd.ip < nd.nins;
                     const bool dpend = (nd.ctl & (C_WAIT | C_DUMPED)) == 0u && nd.ip >= nd.nins;
-                    /* line tags for a hit: RD needs a valid line, WR a line in M or E */
-                    uint32_t kr = 0, kw = 0;
-    #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t lw = s_line[wv][i][lane];
-                        const uint32_t la = lw & 0xFFu, ls = lw >> 16;
-                        kr |= (ls != DT_CI ? la : 0xFFu) << (8 * i);
-                        kw |= (ls <= DT_CE ? la : 0xFFu) << (8 * i);
-                    }
+                    /* line tags for a hit, a byte per line: RD needs a valid line (state != I),
+                     * WR one in M or E (state <= E); 0xFF never equals a 7-bit address */
+                    const uint32_t L0 = s_line[wv][0][lane], L1 = s_line[wv][1][lane];
+                    const uint32_t L2 = s_line[wv][2][lane], L3 = s_line[wv][3][lane];
+                    const uint32_t la4 = __builtin_amdgcn_perm(L1, L0, 0x0C0C0400u) | __builtin_amdgcn_perm(L3, L2, 0x04000C0Cu);
+                    const uint32_t ls4 = __builtin_amdgcn_perm(L1, L0, 0x0C0C0602u) | __builtin_amdgcn_perm(L3, L2, 0x06020C0Cu);
+                    const uint32_t s_or_i = (ls4 >> 1) & 0x01010101u, inv = ls4 & s_or_i;
+                    const uint32_t kr = la4 | ((inv << 8) - inv), kw = la4 | ((s_or_i << 8) - s_or_i);
                     const uint32_t s = nd.ip & 7u, m = 8u - s;
                     uint32_t W[4];
                     if (GEN) {
@@ -561,17 +560,21 @@ sim_kernel(const SimArgs *Ap) {
     #pragma unroll
                         for (int q = 0; q < 4; ++q) W[q] = cur[q] | T[q];
                     }
-                    uint32_t hm = 0;
-    #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const uint32_t h = (W[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                        const uint32_t key = (h & 0x8000u) ? kw : kr;
-                        const uint32_t tag = __builtin_amdgcn_ubfe(key, (h >> 5) & 0x18u, 8);
-                        hm |= (tag == ((h >> 8) & 0x7Fu)) ? (1u << j) : 0u;
-                    }
+                    /* the first miss among the 8, 4 at a time: each instruction's high byte
+                     * (WR << 7 | address) selects its line's tag byte from kw : kr by one byte
+                     * permute; a non-zero byte of tag ^ address is a miss */
+                    auto misses = [&](uint32_t w0, uint32_t w1) -> uint32_t {
+                        const uint32_t hb = __builtin_amdgcn_perm(w1, w0, 0x07050301u);
+                        const uint32_t sel = (hb & 0x03030303u) | ((hb >> 5) & 0x04040404u);
+                        const uint32_t x = __builtin_amdgcn_perm(kw, kr, sel) ^ (hb & 0x7F7F7F7Fu);
+                        return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   /* bit 8j+7 */
+                    };
+                    const uint32_t ma = misses(W[0], W[1]), mb = misses(W[2], W[3]);
+                    const uint32_t run = ma ? (uint32_t)__builtin_ctz(ma) >> 3
+                                            : (mb ? 4u + ((uint32_t)__builtin_ctz(mb) >> 3) : 8u);
                     /* a group with no node issuing makes no progress here */
                     const bool gany = ((__ballot(iss) >> gbase) & NPM) != 0u;
-                    uint32_t r = iss ? (uint32_t)__builtin_ctz(~hm) : (dpend || !gany ? 0u : 8u);
+                    uint32_t r = iss ? run : (dpend || !gany ? 0u : 8u);
                     if (iss && r > nd.nins - nd.ip) r = nd.nins - nd.ip;
                     /* the round limit: the round that reaches it runs normally */
                     if (r > (1u << lim_rsh) - 1u - rounds) r = (1u << lim_rsh) - 1u - rounds;
