@@ -38,6 +38,7 @@
 #include "dsm_table.h"
 #include "dsm_internal.h"
 #include "dsm_gen.h"
+#include "dsm_serial.h"
 
 /* Kernel arguments live in device memory (not the kernarg segment): the hot loop needs
  * almost none of them, and loads from a plain global pointer are not hoisted into SGPRs
@@ -82,6 +83,7 @@ struct SimArgs {
                                      * dsm_set_round_limit): ROUND_LIMIT at that many rounds */
     uint32_t icap;                  /* inbox limit (MSG_BUFFER_SIZE = 256, or
                                      * dsm_set_inbox_limit): RING_OVERFLOW beyond it        */
+    uint32_t susp_ring;             /* resume pass: ring depth of the suspended states       */
 };
 /* the argument blocks of one run, written to device memory by args_kernel (stream-ordered:
  * no pinned staging whose reuse would need a host wait) */
@@ -207,6 +209,8 @@ DEVI uint64_t gsum64(uint64_t x) {
  * counted in both vmcnt and lgkmcnt and completes out of order, so every later wait on it,
  * or on any LDS access, becomes vmcnt(0) lgkmcnt(0). */
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) uint32_t GU32;    /* global (not flat) accesses */
+typedef __attribute__((address_space(1))) v4u32 GV4;
 DEVI uint4 ld16(const uint16_t *p) {
     const v4u32 v = *(const __attribute__((address_space(1))) v4u32 *)p;
     return make_uint4(v.x, v.y, v.z, v.w);
@@ -972,6 +976,236 @@ sim_kernel(const SimArgs *Ap) {
     }
 }
 
+/* ---- resume pass, serial form ------------------------------------------------------------
+ * One lane = one suspended system, taken one node-action per iteration (dsm_serial.h): after
+ * the budget pass the systems still running are almost all one surviving node issuing its
+ * trace while the others wait for good, ~1.3 node-actions per round, so the lock-step
+ * kernel's 8 lanes per system would idle ~84% of the time.  The state of 64 systems sits in
+ * LDS as one column per lane ([word][lane]: every access is conflict-free and private to
+ * its lane, so no barrier or fence is needed); 4 waves of 38 KB fill the CU's 160 KB.  Each
+ * lane takes systems from the suspended list (last-suspended first), restores the lock-step
+ * state (inboxes into SER_D-deep FIFOs), runs it to the end and writes its result and final
+ * records; an inbox deeper than SER_D hands the system to the 256-deep re-run, as a ring
+ * overflow of the lock-step kernel does.  The issuing node's trace chunk and the next one are
+ * kept in registers (refill step below). */
+constexpr int SER_WAVES = 4, SER_D = 4, SER_RF = 4;
+
+template <int W, int NW>
+struct LdsCol {
+    uint32_t (&s)[W][NW][64];
+    uint32_t wv, lane;
+    DEVI uint32_t ld(uint32_t w) const { return s[wv][w][lane]; }
+    DEVI void st(uint32_t w, uint32_t v) const { s[wv][w][lane] = v; }
+    DEVI uint32_t ld16(uint32_t w, uint32_t h) const {
+        return reinterpret_cast<const uint16_t *>(&s[wv][w][lane])[h];
+    }
+    DEVI void st16(uint32_t w, uint32_t h, uint32_t v) const {
+        reinterpret_cast<uint16_t *>(&s[wv][w][lane])[h] = (uint16_t)v;
+    }
+};
+struct LdsTab {
+    const uint2 (&t)[DT_TABLE_WORDS / 2];
+    DEVI uint32_t hdr(uint32_t i) const { return reinterpret_cast<const uint32_t *>(&t[DT_ENTRIES])[i]; }
+    DEVI void row(uint32_t i, uint32_t &w0, uint32_t &w1) const {
+        const uint2 e = t[i];
+        w0 = e.x;
+        w1 = e.y;
+    }
+};
+
+template <int NP>
+__global__ void __launch_bounds__(64 * SER_WAVES) __attribute__((amdgpu_waves_per_eu(1)))
+ser_kernel(const SimArgs *Ap) {
+    using namespace dsms;
+    constexpr uint32_t NW = s_words(SER_D);
+    constexpr uint32_t NPM = (1u << NP) - 1u;
+    /* one of a fast-forward / serial pair: the fast-forward lock-step resume takes the run
+     * when the trace scan picked fast-forward */
+    if (Ap->ffsel && ff_verdict(Ap->scan)) return;
+
+    __shared__ uint32_t s_ser[SER_WAVES][NW][64];
+    __shared__ uint2 s_tab[DT_TABLE_WORDS / 2];
+    __shared__ unsigned long long s_cnt[SER_WAVES][K_N];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    if (lane < K_N) s_cnt[wv][lane] = 0;
+    for (uint32_t i = threadIdx.x; i < DT_TABLE_WORDS / 2; i += 64 * SER_WAVES) s_tab[i] = Ap->table[i];
+    __syncthreads();
+
+    const LdsCol<SER_WAVES, NW> m{s_ser, wv, lane};
+    const LdsTab T{s_tab};
+    const uint32_t n = *Ap->d_n;
+    const uint32_t stride = Ap->stride, lim_rsh = Ap->lim_rsh, SR = Ap->susp_ring;
+    const uint32_t cap = Ap->icap < (uint32_t)SER_D ? Ap->icap : (uint32_t)SER_D;
+    const uint16_t *const traces = Ap->traces;
+
+    /* uniform pointers, hoisted (a wave per SIMD leaves registers to spare) */
+    uint4 *const recs = Ap->recs;
+    dsm_sys_result *const results = Ap->results;
+    const uint32_t *const list = Ap->list;
+    const uint32_t *const susp = Ap->susp;
+    uint32_t *const ovf_list = Ap->ovf_list;
+    unsigned int *const ovf_count = Ap->ovf_count, *const claim_ctr = Ap->claim;
+
+    SReg r;
+    uint64_t sys = 0;
+    /* trace chunks of the node that issues (one at a time, almost always the same node):
+     * cur = chunk tci of node tn, nx = chunk tci + 1 when nxv.  Every prefetch is issued in
+     * the refill step that runs every SER_RF iterations and is taken into nx at the next one,
+     * so a wait on it (the compiler's vmcnt(0)) only ever covers loads issued SER_RF
+     * iterations earlier: a lane that rotates a chunk never stalls the wave on HBM. */
+    uint32_t tn = 0xFFu, tci = 0, pfc = 0;
+    bool nxv = false, pfv = false;
+    uint4 cur = make_uint4(0, 0, 0, 0), nx = cur, pf = cur;
+    auto slot_of = [&](uint32_t nd) { return traces + (sys * NP + nd) * (uint64_t)stride; };
+
+    auto claim = [&]() -> bool {
+        const uint32_t k = atomicAdd(claim_ctr, 1u);
+        if (k >= n) return false;
+        sys = list[n - 1 - k];
+        return true;
+    };
+    /* the lock-step state the budget pass suspended (sim_kernel's layout [word][node]) */
+    auto start = [&]() -> uint32_t {
+        const GU32 *sp = (const GU32 *)(susp + sys * ((uint64_t)susp_words((int)SR) * NP));
+        r.A = r.E = r.nz = r.iss = r.dmp = r.cnt = r.head = 0;
+        r.msgs = r.asrt = r.st = 0;
+        r.rounds = sp[(12u + SR + 6u) * NP];
+        bool deep = false;
+        for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {
+            const GU32 *b = sp + nd;
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) m.st(S_MB + 8u * nd + i, b[i * NP]);
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) m.st(S_LN + 4u * nd + i, b[(8u + i) * NP]);
+            const GU32 *q = b + (12u + SR) * NP;
+            const uint32_t ctl = q[NP], ip = q[2 * NP], rh = q[4 * NP];
+            m.st(S_DS + nd, q[0]);
+            m.st(S_CT + nd, (ctl & 0xFFFFu) | (ip << 16));
+            m.st(S_NI + nd, q[3 * NP]);
+            const uint32_t h = rh & 0xFFu, c = rh >> 8;
+            deep = deep || c > (uint32_t)SER_D;
+#pragma unroll
+            for (uint32_t j = 0; j < (uint32_t)SER_D; ++j) {
+                uint32_t sl = h + j;
+                sl = sl >= SR ? sl - SR : sl;
+                if (j < c) m.st(S_RG + (uint32_t)SER_D * nd + j, b[(12u + sl) * NP]);
+            }
+            r.cnt |= (c < (uint32_t)SER_D ? c : (uint32_t)SER_D) << (4u * nd);
+            r.nz |= (c ? 1u : 0u) << nd;
+            r.msgs += q[5 * NP] - c;       /* received - still queued = handled */
+            r.iss |= ((ctl & (C_WAIT | C_DUMPED)) == 0u ? 1u : 0u) << nd;
+            r.dmp |= ((ctl & C_DUMPED) ? 1u : 0u) << nd;
+        }
+        r.E = r.nz;
+        r.A = r.nz | r.iss;
+        tn = 0xFFu;
+        nxv = pfv = false;
+        if (deep) return SR_OVF;
+        if (r.A == 0u) {
+            r.st = (r.dmp == NPM) ? SS_COMPLETED : SS_DEADLOCKED;
+            return SR_DONE;
+        }
+        return SR_RUN;
+    };
+    auto store_rec = [&](uint32_t nd, uint32_t flags, uint32_t which) {
+        GV4 *dst = (GV4 *)(recs + (sys * NP + nd) * 8 + 4u * which);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            v4u32 x;
+            x.x = ser_rec_word(m, nd, flags, 4 * q);
+            x.y = ser_rec_word(m, nd, flags, 4 * q + 1);
+            x.z = ser_rec_word(m, nd, flags, 4 * q + 2);
+            x.w = ser_rec_word(m, nd, flags, 4 * q + 3);
+            dst[q] = x;
+        }
+    };
+    auto fetch = [&](uint32_t nd, uint32_t ip) -> uint32_t {
+        const uint32_t c = ip >> 3;
+        if (tn != nd || tci != c) {
+            if (tn == nd && tci + 1u == c && nxv) {
+                cur = nx;
+            } else {                       /* another node, or the prefetch not in yet: wait */
+                cur = ld16(slot_of(nd) + 8u * c);
+                pfv = false;
+            }
+            nxv = false;
+            tn = nd;
+            tci = c;
+        }
+        const uint32_t j = ip & 7u;
+        const uint32_t wd = (j & 4u) ? ((j & 2u) ? cur.w : cur.z) : ((j & 2u) ? cur.y : cur.x);
+        return (j & 1u) ? (wd >> 16) : (wd & 0xFFFFu);
+    };
+    auto refill = [&]() {
+        if (pfv && !nxv && pfc == tci + 1u) {      /* issued SER_RF iterations ago */
+            nx = pf;
+            nxv = true;
+        }
+        pfv = false;
+        if (tn != 0xFFu && !nxv) {
+            const uint32_t c1 = tci + 1u;
+            pf = ld16(slot_of(tn) + ((c1 + 1u) * 8u <= stride ? c1 * 8u : stride - 8u));
+            pfc = c1;
+            pfv = true;
+        }
+    };
+    auto on_dump = [&](uint32_t nd) { store_rec(nd, 2u, 0u); };
+    auto finish = [&](uint32_t v) {
+        if (v == SR_OVF) {               /* to the 256-deep re-run, from scratch */
+            const uint32_t pos = atomicAdd(ovf_count, 1u);
+            ovf_list[pos] = (uint32_t)sys;
+            atomicAdd(&s_cnt[wv][K_OVFRERUN], 1ull);
+            return;
+        }
+        uint32_t ins = 0;
+        for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {
+            ins += m.ld(S_CT + nd) >> 16;
+            store_rec(nd, ser_final_flags(m, nd), 1u);
+        }
+        v4u32 res;
+        res.x = r.st | (r.dmp << 8); res.y = r.rounds; res.z = r.msgs; res.w = ins;
+        ((GV4 *)results)[2 * sys] = res;
+        atomicAdd(&s_cnt[wv][K_MSGS], (unsigned long long)r.msgs);
+        atomicAdd(&s_cnt[wv][K_INSTRS], (unsigned long long)ins);
+        atomicAdd(&s_cnt[wv][K_ROUNDS], (unsigned long long)r.rounds);
+        atomicAdd(&s_cnt[wv][K_SYSTEMS], 1ull);
+        atomicAdd(&s_cnt[wv][K_STATUS + r.st], 1ull);
+        atomicMax(&s_cnt[wv][K_MAXR], (unsigned long long)r.rounds);
+    };
+
+    bool live = claim();
+    uint32_t v = live ? start() : SR_RUN;
+    uint32_t iters = 0;
+    for (;;) {
+#pragma unroll 1
+        for (int k = 0; k < SER_RF; ++k) {
+            if (live && v == SR_RUN) v = ser_step<NP, SER_D>(m, r, T, fetch, on_dump, lim_rsh, cap);
+            if (live && v != SR_RUN) {
+                finish(v);
+                live = claim();
+                v = live ? start() : SR_RUN;
+            }
+        }
+        refill();
+        iters += SER_RF;
+        if (__ballot(live) == 0) break;
+    }
+    if (lane == 0) s_cnt[wv][K_WROUNDS] = iters;
+    __syncthreads();
+    if (threadIdx.x < K_N) {
+        unsigned long long x = s_cnt[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < SER_WAVES; ++w) {
+            const unsigned long long y = s_cnt[w][threadIdx.x];
+            x = threadIdx.x == K_MAXR ? (y > x ? y : x) : x + y;
+        }
+        if (x) {
+            if (threadIdx.x == K_MAXR) atomicMax(&Ap->counters[K_MAXR], x);
+            else atomicAdd(&Ap->counters[threadIdx.x], x);
+        }
+    }
+}
+
 /* ---- digest: per-system hashes of the node records ------------------------------------
  * One lane per node record pair; dump_hash sums the 15-word hash of every dumped node's
  * dump record, final_hash the 16-word hash of every final record.  Memory-
@@ -1214,6 +1448,7 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->round_limit_log2 = RSH_MAX;
     c->inbox_limit = FB_RING;
     c->ff_mode = DSM_FF_AUTO;
+    c->serial = (int)env_u32("DSM_SERIAL", 1);
     c->fmt_tile = (int)env_u32("DSM_FMT", 132);
     c->parse_bpl = (int)env_u32("DSM_PARSE_BPL", 32);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -1324,6 +1559,10 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     if (dblocks > (uint64_t)c->cus * 8) dblocks = (uint64_t)c->cus * 8;
     /* two-pass schedule on the packed path in bench mode */
     const uint32_t blog = ((mode & ~M_LIM) == 0 && !gen) ? c->budget_log2 : 0u;
+    /* the resume pass in serial form (ser_kernel) unless fast-forward is forced; with the
+     * fast-forward pair, the trace scan's verdict picks between it and the fast-forward
+     * lock-step resume */
+    const bool use_ser = blog && c->serial && c->ff_mode != DSM_FF_ON;
     int rc;
     if ((rc = ensure(&c->d_ovf_list, &c->ovf_cap, (size_t)n_sys))) return rc;
     const int ring_eff = (mode && c->ring != 4) ? 12 : c->ring;   /* fast_mode's choice */
@@ -1374,6 +1613,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.susp = c->d_susp;
     A.susp_list = c->d_susp_list;
     A.susp_count = c->d_ctrl + CTRL_SUSP;
+    A.susp_ring = (uint32_t)ring_eff;
     if (tr) {
         A.issue = c->d_issue;
         A.issue_n = c->d_issue_n;
@@ -1421,11 +1661,18 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
         HIPCK(hipGetLastError());
     }
     for (int pass = 0; pass < (blog ? 2 : 1); ++pass) {
-        /* resume pass at the budget pass's grid: it sizes itself from the suspended count */
+        /* resume pass at the budget pass's grid: it sizes itself from the suspended count;
+         * in serial form (ser_kernel) one workgroup per CU, one system per lane */
         const SimArgs *a = (const SimArgs *)(c->d_args + 2 * pass);
-        hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, a);
-        HIPCK(hipGetLastError());
-        if (pair) {
+        const bool ser = pass == 1 && use_ser;
+        if (!ser || pair) {
+            hipLaunchKernelGGL(fast, dim3(grid_fast), dim3(64 * FW), 0, st, a);
+            HIPCK(hipGetLastError());
+        }
+        if (ser) {
+            hipLaunchKernelGGL(np == 4 ? ser_kernel<4> : ser_kernel<8>, dim3(c->cus), dim3(64 * SER_WAVES), 0, st, a);
+            HIPCK(hipGetLastError());
+        } else if (pair) {
             hipLaunchKernelGGL(fast_nf, dim3(grid_fast), dim3(64 * FW), 0, st, a);
             HIPCK(hipGetLastError());
         }
@@ -1452,7 +1699,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     c->info.waves_per_cu = nb_fast * FW;
     c->info.cus = c->cus;
     c->info.ring_cap = ring_eff;
-    c->info.resume_blocks = blog ? grid_fast : 0;
+    c->info.resume_blocks = blog ? (use_ser ? c->cus : grid_fast) : 0;
     c->info.budget_log2 = (int)blog;
     c->info.lds_bytes_per_block = lds_bytes(ring_eff, FW);
     c->info.late_log2 = (int)A.late_rsh;

@@ -48,6 +48,7 @@ struct dsm_ctx {
      * DSM_BUDGET_LOG2 / DSM_LATE_LOG2, read once at dsm_open) */
     uint32_t budget_log2, late_log2, round_limit_log2, inbox_limit;
     int ff_mode;                       /* DSM_FF_OFF / ON / AUTO */
+    int serial;                        /* resume pass in serial form (ser_kernel; DSM_SERIAL) */
     /* dsm_text.hip tuning (DSM_FMT / DSM_PARSE_BPL, read once at dsm_open) */
     int fmt_tile, parse_bpl;
     uint64_t sched_seed;             /* dsm_set_schedule                                     */

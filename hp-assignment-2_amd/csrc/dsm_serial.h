@@ -1,0 +1,226 @@
+/*
+ * dsm_serial.h -- the lock-step round taken one node-action at a time: one lane (or one host
+ * loop) simulates a whole system.  Used by the resume pass of the two-pass schedule
+ * (dsm_engine.hip ser_kernel) and by a host model that checks it against the oracle
+ * (tests/model/serial_model.cpp).
+ *
+ * Why: after a few thousand rounds a C3 system is one surviving node issuing its trace while
+ * the others wait forever (the home has no transient states,
+ * assignment.c:265-270, :467-472), ~1.3 node-actions per round.  The lock-step kernel runs
+ * such a system on 8 lanes of which ~1.3 act; here every lane acts in every iteration.
+ *
+ * Schedule, restated for one node at a time.  In each round every node
+ * takes one action decided from its state at the start of the round (inbox head, else idle
+ * if waiting, else issue, else dump once); sends are appended at the end of the round in
+ * ascending sender order, then program order.  Nodes are taken in ascending order here and
+ * a send is appended to the receiver's inbox at once.  That is the same thing, because
+ *   - a node's action reads and writes only its own state (assignment.c :157-697: directory,
+ *     memory, cache and control of threadId) and appends to other inboxes (sendMessage
+ *     :711-739), so the nodes of one round commute but for those appends;
+ *   - the appends reach every receiver in (sender, program order), as at the end of the
+ *     round;
+ *   - a receiver decides from the inbox it had at the start of the round (mask E): an append
+ *     goes to the tail, so the head it pops is the one it had, and a node whose inbox was
+ *     empty at the start does not pop what arrived during the round.
+ * A round in which no node has an action ends the system (`rounds` counts the active ones).
+ *
+ * Inboxes are D-deep FIFOs here (the analysis in DESIGN.md: after round 2^12 a C3 inbox
+ * holds at most 2 messages at any moment in 99.9% of systems).  An append to a full FIFO
+ * ends the system's run here with SR_OVF: the caller hands the system to the 256-deep
+ * re-run from scratch, as the lock-step kernel does with its ring overflows, so results never
+ * depend on D.
+ */
+#ifndef DSM_SERIAL_H
+#define DSM_SERIAL_H
+
+#include "dsm_table.h"
+
+namespace dsms {
+
+/* per-system words (one LDS column per lane on the device, a plain array on the host):
+ *   S_MB + 8n + p   node n, blocks 2p and 2p+1: memory | bitVector << 8 per 16-bit half
+ *   S_LN + 4n + i   node n, cache line i: address | value << 8 | state << 16
+ *   S_DS + n        node n, directory states (2 bits per block)
+ *   S_CT + n        node n, pendingWriteValue | flags << 8 | instructions issued << 16
+ *   S_NI + n        node n, instructions in its trace
+ *   S_RG + Dn + j   node n, inbox slot j (ring entries: body | sender << 24)           */
+enum : uint32_t { S_MB = 0, S_LN = 64, S_DS = 96, S_CT = 104, S_NI = 112, S_RG = 120 };
+constexpr uint32_t s_words(int D) { return S_RG + 8u * (uint32_t)D; }
+
+/* control bits (the lock-step kernel's C_*): wait 8, dumped 9, assert 11 */
+enum : uint32_t { SC_WAIT = DT_CTL_WAIT, SC_DUMPED = 1u << 9, SC_ASSERT = DT_CTL_ASSERT };
+enum : uint32_t { SR_RUN = 0, SR_DONE = 1, SR_OVF = 2 };          /* ser_step verdicts */
+/* statuses (include/dsm.h DSM_*) */
+enum : uint32_t { SS_COMPLETED = 0, SS_DEADLOCKED = 1, SS_ASSERT = 3, SS_ROUND_LIMIT = 4 };
+constexpr uint32_t S_LINE_INIT = 0xFFu | (3u << 16);   /* address 0xFF, value 0, INVALID */
+
+/* a system's registers */
+struct SReg {
+    uint32_t A;       /* nodes still to act in this round                                   */
+    uint32_t E;       /* nodes whose inbox was non-empty at the start of this round         */
+    uint32_t nz;      /* nodes whose inbox is non-empty now                                 */
+    uint32_t iss;     /* nodes neither waiting nor dumped: they issue, or dump, next        */
+    uint32_t dmp;     /* nodes that dumped                                                   */
+    uint32_t cnt;     /* inbox counts, a nibble per node                                    */
+    uint32_t head;    /* inbox heads, a nibble per node                                     */
+    uint32_t rounds;  /* active rounds                                                      */
+    uint32_t msgs;    /* messages handled                                                   */
+    uint32_t asrt;    /* an assert fired in this round                                      */
+    uint32_t st;      /* status once SR_DONE                                                */
+};
+
+DSM_HD uint32_t s_nib(uint32_t w, uint32_t n) { return (w >> (4u * n)) & 15u; }
+DSM_HD uint32_t s_get2(uint32_t w, uint32_t i) { return dt_ubfe(w, 2u * i, 2u); }
+DSM_HD uint32_t s_set2(uint32_t w, uint32_t i, uint32_t v) {
+    const uint32_t sh = 2u * i;
+    return (w & ~(3u << sh)) | (v << sh);
+}
+DSM_HD uint32_t s_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
+
+/* a fresh system: initializeProcessor :778-790 and main :142-146 for every node */
+template <int NP, class M>
+DSM_HD void ser_fresh(M &m, SReg &r, const uint32_t *counts, uint32_t stride) {
+    for (uint32_t n = 0; n < (uint32_t)NP; ++n) {
+        for (uint32_t p = 0; p < 8; ++p)
+            m.st(S_MB + 8 * n + p, ((20u * n + 2 * p) & 0xFFu) | (((20u * n + 2 * p + 1) & 0xFFu) << 16));
+        for (uint32_t i = 0; i < 4; ++i) m.st(S_LN + 4 * n + i, S_LINE_INIT);
+        m.st(S_DS + n, 0xAAAAAAAAu);                       /* every block UNOWNED */
+        m.st(S_CT + n, 0u);
+        m.st(S_NI + n, counts[n] < stride ? counts[n] : stride);
+    }
+    r.A = r.iss = (1u << NP) - 1u;
+    r.E = r.nz = r.dmp = r.cnt = r.head = 0;
+    r.rounds = r.msgs = r.asrt = r.st = 0;
+}
+
+/* one node-action of the system (the lowest node left in this round), then, if it was the
+ * round's last, the end of the round.  F fetch(node, index) -> packed instruction;
+ * R on_dump(node): the node's dump record is due (state as stored, flags 2).  An append
+ * that would make an inbox hold more than cap (<= D) messages ends the run with SR_OVF. */
+template <int NP, int D, class M, class T, class F, class R>
+DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, uint32_t lim_rsh,
+                         uint32_t cap = (uint32_t)D) {
+    constexpr uint32_t NPM = (1u << NP) - 1u;
+    const uint32_t n = s_ctz(r.A);
+    uint32_t ct = m.ld(S_CT + n);
+    const uint32_t nins = m.ld(S_NI + n);
+    const uint32_t h0 = s_nib(r.head, n);
+    const uint32_t rw = m.ld(S_RG + (uint32_t)D * n + h0);     /* inbox head (may be stale) */
+    const bool hasMsg = (r.E >> n) & 1u;                          /* :158-169 */
+    const bool doIssue = !hasMsg && (ct >> 16) < nins;            /* :590-592 */
+    const bool doDump = !hasMsg && !doIssue;                      /* :688-697 */
+    uint32_t w = rw;
+    if (hasMsg) {
+        const uint32_t hn = (h0 + 1u == (uint32_t)D) ? 0u : h0 + 1u;
+        r.head = (r.head & ~(15u << (4u * n))) | (hn << (4u * n));
+        r.cnt -= 1u << (4u * n);
+        if (s_nib(r.cnt, n) == 0u) r.nz &= ~(1u << n);
+        r.msgs++;
+    } else if (doIssue) {
+        w = dt_issue_word(fetch(n, ct >> 16));
+        ct += 1u << 16;
+    }
+    const uint32_t op = doDump ? (uint32_t)DT_DUMP : dt_type(w);
+
+    /* decode + micro-op table + datapath (dsm_table.h), as in sim_kernel step (2)-(3) */
+    DtIn in;
+    dt_decode(w, &in.a, &in.v, &in.excl, &in.r2, &in.s);
+    const uint32_t blk = in.a & 15u, idx = in.a & 3u;            /* :177-184 */
+    const uint32_t mw = S_MB + 8u * n + (blk >> 1);
+    const uint32_t mbw = m.ld16(mw, blk & 1u);
+    const uint32_t lw = m.ld(S_LN + 4u * n + idx);
+    const uint32_t dsw = m.ld(S_DS + n);
+    in.op = op; in.node = n; in.np_mask = NPM;
+    in.La = lw & 0xFFu; in.Lv = (lw >> 8) & 0xFFu; in.Ls = lw >> 16;
+    in.Db = mbw >> 8; in.Ds = s_get2(dsw, blk); in.Mv = mbw & 0xFFu; in.pend = ct & 0xFFu;
+    uint32_t hix = op | ((in.a >> 4) == n ? 32u : 0u);
+    if (NP < 8) hix = (op == DT_RD && (in.a >> 4) >= (uint32_t)NP) ? (uint32_t)DT_ASSERT : hix;
+    uint32_t evDb;
+    const uint32_t ti = dt_index(in, tab.hdr(hix), &evDb);
+    uint32_t W0, W1;
+    tab.row(ti, W0, W1);
+    const uint32_t X = dt_perm(lw, w, 0x05040001u) & ~0x80u;
+    const uint32_t Y = dt_perm(mbw, ct, 0x0C050400u) | ((evDb & 0xFFu) << 24);
+    const DtOut o = dt_apply_xy(in, X, Y, W0, W1, evDb);
+    m.st(S_LN + 4u * n + idx, dt_perm(o.S, o.P, 0x0C040100u));   /* nLa nLv nLs */
+    m.st(S_DS + n, s_set2(dsw, blk, o.nDs));
+    m.st16(mw, blk & 1u, o.nMv | (o.nDb << 8));
+    ct = (ct & ~o.cclr) | o.cset;            /* wait, pendingWriteValue (:633), assert */
+    if (doDump) {
+        ct |= SC_DUMPED;                     /* printProcessorState(threadId, node), :695 */
+        r.dmp |= 1u << n;
+    }
+    m.st(S_CT + n, ct);
+    if (doDump) on_dump(n);
+    r.iss = (ct & (SC_WAIT | SC_DUMPED)) ? (r.iss & ~(1u << n)) : (r.iss | (1u << n));
+    r.asrt |= ct & SC_ASSERT;
+
+    /* sendMessage :711-739: the first word (to its destinations in ascending order), then the
+     * second; each to the tail of the receiver's inbox */
+    bool ovf = false;
+    const uint32_t ow[2] = {o.o0, o.o1};
+    for (int j = 0; j < 2; ++j) {
+        uint32_t dm = ow[j] >> 24;
+        const uint32_t e = dt_ring_entry(ow[j], n);
+        while (dm) {
+            const uint32_t d = s_ctz(dm);
+            dm &= dm - 1u;
+            const uint32_t c = s_nib(r.cnt, d);
+            ovf = ovf || c >= cap;
+            uint32_t slot = s_nib(r.head, d) + c;
+            slot = slot >= (uint32_t)D ? slot - (uint32_t)D : slot;
+            if (c < (uint32_t)D) m.st(S_RG + (uint32_t)D * d + slot, e);
+            r.cnt += c < (uint32_t)D ? 1u << (4u * d) : 0u;
+            r.nz |= 1u << d;
+        }
+    }
+    if (ovf) return SR_OVF;
+
+    r.A &= ~(1u << n);
+    if (r.A) return SR_RUN;
+    /* ---- end of the round (Appendix A step 4) ---- */
+    r.rounds++;
+    if (r.asrt) { r.st = SS_ASSERT; return SR_DONE; }            /* a failed assert */
+    if (r.rounds >> lim_rsh) { r.st = SS_ROUND_LIMIT; return SR_DONE; }
+    r.E = r.nz;
+    r.A = r.nz | r.iss;
+    if (r.A == 0u) {                                           /* quiescent */
+        r.st = (r.dmp == NPM) ? SS_COMPLETED : SS_DEADLOCKED;
+        return SR_DONE;
+    }
+    return SR_RUN;
+}
+
+/* word i of node n's canonical 64-byte record (dsm_node_state); flags = wait | dumped << 1 */
+template <class M>
+DSM_HD uint32_t ser_rec_word(M &m, uint32_t n, uint32_t flags, int i) {
+    if (i < 8) {                        /* memory bytes (words 0-3), bitVector bytes (4-7) */
+        const uint32_t k = (uint32_t)i & 3u;
+        const uint32_t x = m.ld(S_MB + 8u * n + 2u * k), y = m.ld(S_MB + 8u * n + 2u * k + 1u);
+        return dt_perm(y, x, i < 4 ? 0x06040200u : 0x07050301u);
+    }
+    if (i < 12) {                       /* directory states, a byte per block */
+        const uint32_t e = m.ld(S_DS + n) >> (8 * (i - 8));
+        return (e & 3u) | (((e >> 2) & 3u) << 8) | (((e >> 4) & 3u) << 16) | (((e >> 6) & 3u) << 24);
+    }
+    if (i < 15) {                       /* cache addresses / values / states */
+        const uint32_t b = (uint32_t)(i - 12);
+        const uint32_t sel = 0x0C0C0400u | (b * 0x00000101u);
+        const uint32_t l0 = m.ld(S_LN + 4u * n), l1 = m.ld(S_LN + 4u * n + 1u);
+        const uint32_t l2 = m.ld(S_LN + 4u * n + 2u), l3 = m.ld(S_LN + 4u * n + 3u);
+        return dt_perm(dt_perm(l3, l2, sel), dt_perm(l1, l0, sel), 0x05040100u);
+    }
+    const uint32_t ct = m.ld(S_CT + n);
+    return (ct & 0xFFu) | (flags << 8) | (ct & 0xFFFF0000u);
+}
+
+/* record flags of node n at the end: waitingForReply | dumped << 1 */
+template <class M>
+DSM_HD uint32_t ser_final_flags(M &m, uint32_t n) {
+    const uint32_t ct = m.ld(S_CT + n);
+    return ((ct & SC_WAIT) ? 1u : 0u) | ((ct & SC_DUMPED) ? 2u : 0u);
+}
+
+}  // namespace dsms
+
+#endif

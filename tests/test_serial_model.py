@@ -1,0 +1,47 @@
+"""The serial form of the lock-step round (hp-assignment-2_amd/csrc/dsm_serial.h, the resume
+pass's per-lane engine) on the host, whole systems from their first round, against the
+oracle (tests/model/serial_model.cpp): results, rounds, records (as hashes) bit-exact; the
+systems whose inbox would outgrow the FIFO are counted (the kernel hands them to the
+256-deep re-run)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+
+@pytest.fixture(scope="module")
+def serial_model(tmp_path_factory):
+    d = tmp_path_factory.mktemp("ser")
+    obj = str(d / "orc.o")
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-c", os.path.join(REPO, "oracle", "dsm_oracle.c"),
+                    "-I", os.path.join(REPO, "oracle"), "-o", obj], check=True)
+    exe = str(d / "serial_model")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fopenmp",
+                    "-I", os.path.join(REPO, "oracle"),
+                    "-I", os.path.join(REPO, "hp-assignment-2_amd", "csrc"),
+                    os.path.join(REPO, "tests", "model", "serial_model.cpp"), obj, "-o", exe],
+                   check=True)
+    return exe
+
+
+# np, dist (3: 8-node addresses on 4 nodes -> ASSERT_FAILED), systems, FIFO depth,
+# round limit log2 (0: default), instructions per node
+CASES = [(8, 0, 1500, 8, 0, 4096), (8, 1, 600, 8, 0, 4096), (8, 2, 1500, 8, 0, 4096),
+         (8, 0, 1500, 4, 0, 4096), (8, 2, 1500, 4, 0, 4096), (4, 0, 2000, 4, 0, 4096),
+         (4, 3, 1000, 8, 0, 256), (8, 0, 800, 8, 9, 4096), (4, 1, 500, 8, 8, 4096)]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"np{c[0]}_d{c[1]}_D{c[3]}_lim{c[4]}" for c in CASES])
+def test_serial_engine_matches_oracle(serial_model, case):
+    r = subprocess.run([serial_model] + [str(x) for x in case], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["compared"] + d["ovf"] == d["systems"] and d["compared"] > d["systems"] // 5
+    if case[1] == 3:
+        assert d["by_status"][3] > 0
+    if case[4]:
+        assert d["by_status"][4] > 0
