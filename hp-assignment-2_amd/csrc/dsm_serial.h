@@ -43,9 +43,10 @@ namespace dsms {
  *   S_DS + n        node n, directory states (2 bits per block)
  *   S_CT + n        node n, pendingWriteValue | flags << 8 | instructions issued << 16
  *   S_NI + n        node n, instructions in its trace
- *   S_RG + Dn + j   node n, inbox slot j (ring entries: body | sender << 24)           */
+ *   S_RG + Dn + j   node n, inbox slot j (ring entries: body | sender << 24)
+ *   S_RG + 8D       scratch: the target of a disabled (predicated-off) append          */
 enum : uint32_t { S_MB = 0, S_LN = 64, S_DS = 96, S_CT = 104, S_NI = 112, S_RG = 120 };
-constexpr uint32_t s_words(int D) { return S_RG + 8u * (uint32_t)D; }
+constexpr uint32_t s_words(int D) { return S_RG + 8u * (uint32_t)D + 1u; }   /* + scratch */
 
 /* control bits (the lock-step kernel's C_*): wait 8, dumped 9, assert 11 */
 enum : uint32_t { SC_WAIT = DT_CTL_WAIT, SC_DUMPED = 1u << 9, SC_ASSERT = DT_CTL_ASSERT };
@@ -94,32 +95,36 @@ DSM_HD void ser_fresh(M &m, SReg &r, const uint32_t *counts, uint32_t stride) {
 }
 
 /* one node-action of the system (the lowest node left in this round), then, if it was the
- * round's last, the end of the round.  F fetch(node, index) -> packed instruction;
- * R on_dump(node): the node's dump record is due (state as stored, flags 2).  An append
- * that would make an inbox hold more than cap (<= D) messages ends the run with SR_OVF. */
+ * round's last, the end of the round.  Branch-free but for the dump record and the rare
+ * third-and-later destinations of a multicast: on the device every lane of a wave runs a
+ * different system, and divergent branches cost more than the predicated work.
+ *   F fetch(node, index, issue) -> the packed instruction (only used when issue);
+ *   R on_dump(node): the node's dump record is due (state as stored, flags 2).
+ * An append that would make an inbox hold more than cap (<= D) messages ends the run with
+ * SR_OVF.  A disabled append writes the scratch word S_RG + 8D. */
 template <int NP, int D, class M, class T, class F, class R>
 DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, uint32_t lim_rsh,
                          uint32_t cap = (uint32_t)D) {
-    constexpr uint32_t NPM = (1u << NP) - 1u;
-    const uint32_t n = s_ctz(r.A);
+    constexpr uint32_t NPM = (1u << NP) - 1u, SCR = S_RG + 8u * (uint32_t)D;
+    const uint32_t n = s_ctz(r.A), n4 = 4u * n, bit = 1u << n;
     uint32_t ct = m.ld(S_CT + n);
     const uint32_t nins = m.ld(S_NI + n);
     const uint32_t h0 = s_nib(r.head, n);
-    const uint32_t rw = m.ld(S_RG + (uint32_t)D * n + h0);     /* inbox head (may be stale) */
-    const bool hasMsg = (r.E >> n) & 1u;                          /* :158-169 */
+    const uint32_t rw = m.ld(S_RG + (uint32_t)D * n + h0);      /* inbox head (may be stale) */
+    const bool hasMsg = (r.E & bit) != 0u;                        /* :158-169 */
     const bool doIssue = !hasMsg && (ct >> 16) < nins;            /* :590-592 */
     const bool doDump = !hasMsg && !doIssue;                      /* :688-697 */
-    uint32_t w = rw;
-    if (hasMsg) {
+    const uint32_t ins = fetch(n, ct >> 16, doIssue);
+    const uint32_t w = hasMsg ? rw : dt_issue_word(ins);
+    {   /* pop the head */
         const uint32_t hn = (h0 + 1u == (uint32_t)D) ? 0u : h0 + 1u;
-        r.head = (r.head & ~(15u << (4u * n))) | (hn << (4u * n));
-        r.cnt -= 1u << (4u * n);
-        if (s_nib(r.cnt, n) == 0u) r.nz &= ~(1u << n);
-        r.msgs++;
-    } else if (doIssue) {
-        w = dt_issue_word(fetch(n, ct >> 16));
-        ct += 1u << 16;
+        const uint32_t nh = (r.head & ~(15u << n4)) | (hn << n4);
+        r.head = hasMsg ? nh : r.head;
+        r.cnt -= hasMsg ? (1u << n4) : 0u;
+        r.nz &= (hasMsg && s_nib(r.cnt, n) == 0u) ? ~bit : ~0u;
+        r.msgs += hasMsg ? 1u : 0u;
     }
+    ct += doIssue ? (1u << 16) : 0u;
     const uint32_t op = doDump ? (uint32_t)DT_DUMP : dt_type(w);
 
     /* decode + micro-op table + datapath (dsm_table.h), as in sim_kernel step (2)-(3) */
@@ -145,40 +150,45 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
     m.st(S_LN + 4u * n + idx, dt_perm(o.S, o.P, 0x0C040100u));   /* nLa nLv nLs */
     m.st(S_DS + n, s_set2(dsw, blk, o.nDs));
     m.st16(mw, blk & 1u, o.nMv | (o.nDb << 8));
-    ct = (ct & ~o.cclr) | o.cset;            /* wait, pendingWriteValue (:633), assert */
-    if (doDump) {
-        ct |= SC_DUMPED;                     /* printProcessorState(threadId, node), :695 */
-        r.dmp |= 1u << n;
-    }
+    ct = (ct & ~o.cclr) | o.cset | (doDump ? SC_DUMPED : 0u);   /* wait, pending (:633), assert */
     m.st(S_CT + n, ct);
-    if (doDump) on_dump(n);
-    r.iss = (ct & (SC_WAIT | SC_DUMPED)) ? (r.iss & ~(1u << n)) : (r.iss | (1u << n));
+    r.dmp |= doDump ? bit : 0u;
+    if (doDump) on_dump(n);                  /* printProcessorState(threadId, node), :695 */
+    r.iss = (ct & (SC_WAIT | SC_DUMPED)) ? (r.iss & ~bit) : (r.iss | bit);
     r.asrt |= ct & SC_ASSERT;
 
-    /* sendMessage :711-739: the first word (to its destinations in ascending order), then the
+    /* sendMessage :711-739: the first word to its destinations in ascending order, then the
      * second; each to the tail of the receiver's inbox */
     bool ovf = false;
-    const uint32_t ow[2] = {o.o0, o.o1};
-    for (int j = 0; j < 2; ++j) {
-        uint32_t dm = ow[j] >> 24;
-        const uint32_t e = dt_ring_entry(ow[j], n);
-        while (dm) {
-            const uint32_t d = s_ctz(dm);
+    auto append = [&](bool en, uint32_t d, uint32_t e) {
+        const uint32_t c = s_nib(r.cnt, d);
+        const bool ok = en && c < cap;
+        ovf = ovf || (en && c >= cap);
+        uint32_t slot = s_nib(r.head, d) + c;
+        slot = slot >= (uint32_t)D ? slot - (uint32_t)D : slot;
+        m.st(ok ? S_RG + (uint32_t)D * d + slot : SCR, e);
+        r.cnt += ok ? 1u << (4u * d) : 0u;
+        r.nz |= ok ? 1u << d : 0u;
+    };
+    {
+        uint32_t dm = o.o0 >> 24;
+        const uint32_t e0 = dt_ring_entry(o.o0, n);
+        append(dm != 0u, s_ctz(dm | 0x100u) & 7u, e0);          /* first destination  */
+        dm &= dm - 1u;
+        append(dm != 0u, s_ctz(dm | 0x100u) & 7u, e0);          /* second (FLUSH: home + requester) */
+        dm &= dm - 1u;
+        while (dm) {                                              /* an INV multicast    */
+            append(true, s_ctz(dm), e0);
             dm &= dm - 1u;
-            const uint32_t c = s_nib(r.cnt, d);
-            ovf = ovf || c >= cap;
-            uint32_t slot = s_nib(r.head, d) + c;
-            slot = slot >= (uint32_t)D ? slot - (uint32_t)D : slot;
-            if (c < (uint32_t)D) m.st(S_RG + (uint32_t)D * d + slot, e);
-            r.cnt += c < (uint32_t)D ? 1u << (4u * d) : 0u;
-            r.nz |= 1u << d;
         }
+        const uint32_t d1 = o.o1 >> 24;
+        append(d1 != 0u, s_ctz(d1 | 0x100u) & 7u, dt_ring_entry(o.o1, n));
     }
-    if (ovf) return SR_OVF;
 
-    r.A &= ~(1u << n);
-    if (r.A) return SR_RUN;
     /* ---- end of the round (Appendix A step 4) ---- */
+    r.A &= ~bit;
+    if (ovf) return SR_OVF;
+    if (r.A) return SR_RUN;
     r.rounds++;
     if (r.asrt) { r.st = SS_ASSERT; return SR_DONE; }            /* a failed assert */
     if (r.rounds >> lim_rsh) { r.st = SS_ROUND_LIMIT; return SR_DONE; }

@@ -79,7 +79,7 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr) {
         dsms::ser_fresh<NP>(m, r, counts.data() + s * NP, stride);
         dsm_rec dump[8];
         memset(dump, 0, sizeof dump);
-        auto fetch = [&](uint32_t n, uint32_t i) -> uint32_t { return tr[(size_t)n * stride + i]; };
+        auto fetch = [&](uint32_t n, uint32_t i, bool iss) -> uint32_t { return iss ? tr[(size_t)n * stride + i] : 0u; };
         auto on_dump = [&](uint32_t n) { to_rec(m, n, 2u, &dump[n]); };
         uint32_t v;
         do {
