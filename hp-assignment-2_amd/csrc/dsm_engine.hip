@@ -84,6 +84,7 @@ struct SimArgs {
     uint32_t icap;                  /* inbox limit (MSG_BUFFER_SIZE = 256, or
                                      * dsm_set_inbox_limit): RING_OVERFLOW beyond it        */
     uint32_t susp_ring;             /* resume pass: ring depth of the suspended states       */
+    uint32_t *spill;                /* serial resume: [lane][node][256] inbox spill FIFOs    */
 };
 /* the argument blocks of one run, written to device memory by args_kernel (stream-ordered:
  * no pinned staging whose reuse would need a host wait) */
@@ -985,9 +986,9 @@ sim_kernel(const SimArgs *Ap) {
  * LDS as one column per lane ([word][lane]: every access is conflict-free and private to
  * its lane, so no barrier or fence is needed); 4 waves of 38 KB fill the CU's 160 KB.  Each
  * lane takes systems from the suspended list (last-suspended first), restores the lock-step
- * state (inboxes into SER_D-deep FIFOs), runs it to the end and writes its result and final
- * records; an inbox deeper than SER_D hands the system to the 256-deep re-run, as a ring
- * overflow of the lock-step kernel does.  The issuing node's trace chunk and the next one are
+ * state (inboxes into SER_D-deep FIFOs, continued in the lane's spill FIFOs in HBM), runs it
+ * to the end and writes its result and final records; only an inbox beyond the inbox limit
+ * hands the system to the 256-deep re-run, as a ring overflow of the lock-step kernel does.  The issuing node's trace chunk and the next one are
  * kept in registers (refill step below). */
 constexpr int SER_WAVES = 4, SER_D = 4, SER_RF = 16;
 
@@ -995,6 +996,7 @@ template <int W, int NW>
 struct LdsCol {
     uint32_t (&s)[W][NW][64];
     uint32_t wv, lane;
+    GU32 *sp;                             /* this lane's spill FIFOs, 256 words per node */
     DEVI uint32_t ld(uint32_t w) const { return s[wv][w][lane]; }
     DEVI void st(uint32_t w, uint32_t v) const { s[wv][w][lane] = v; }
     DEVI uint32_t ld16(uint32_t w, uint32_t h) const {
@@ -1003,6 +1005,8 @@ struct LdsCol {
     DEVI void st16(uint32_t w, uint32_t h, uint32_t v) const {
         reinterpret_cast<uint16_t *>(&s[wv][w][lane])[h] = (uint16_t)v;
     }
+    DEVI uint32_t sp_ld(uint32_t d, uint32_t i) const { return sp[d * 256u + i]; }
+    DEVI void sp_st(uint32_t d, uint32_t i, uint32_t v) const { sp[d * 256u + i] = v; }
 };
 struct LdsTab {
     const uint2 (&t)[DT_TABLE_WORDS / 2];
@@ -1032,11 +1036,12 @@ ser_kernel(const SimArgs *Ap) {
     for (uint32_t i = threadIdx.x; i < DT_TABLE_WORDS / 2; i += 64 * SER_WAVES) s_tab[i] = Ap->table[i];
     __syncthreads();
 
-    const LdsCol<SER_WAVES, NW> m{s_ser, wv, lane};
+    const LdsCol<SER_WAVES, NW> m{s_ser, wv, lane,
+                                  (GU32 *)(Ap->spill + ((uint64_t)blockIdx.x * (64 * SER_WAVES) + threadIdx.x) * (8u * 256u))};
     const LdsTab T{s_tab};
     const uint32_t n = *Ap->d_n;
     const uint32_t stride = Ap->stride, lim_rsh = Ap->lim_rsh, SR = Ap->susp_ring;
-    const uint32_t cap = Ap->icap < (uint32_t)SER_D ? Ap->icap : (uint32_t)SER_D;
+    const uint32_t cap = Ap->icap;
     const uint16_t *const traces = Ap->traces;
 
     /* uniform pointers, hoisted (a wave per SIMD leaves registers to spare) */
@@ -1071,8 +1076,8 @@ ser_kernel(const SimArgs *Ap) {
         const GU32 *sp = (const GU32 *)(susp + sys * ((uint64_t)susp_words((int)SR) * NP));
         r.A = r.E = r.nz = r.iss = r.dmp = r.cnt = r.head = 0;
         r.msgs = r.asrt = r.st = 0;
+        r.spl = r.sc0 = r.sc1 = r.sh0 = r.sh1 = 0;
         r.rounds = sp[(12u + SR + 6u) * NP];
-        bool deep = false;
         for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {
             const GU32 *b = sp + nd;
 #pragma unroll
@@ -1085,12 +1090,16 @@ ser_kernel(const SimArgs *Ap) {
             m.st(S_CT + nd, (ctl & 0xFFFFu) | (ip << 16));
             m.st(S_NI + nd, q[3 * NP]);
             const uint32_t h = rh & 0xFFu, c = rh >> 8;
-            deep = deep || c > (uint32_t)SER_D;
-#pragma unroll
-            for (uint32_t j = 0; j < (uint32_t)SER_D; ++j) {
+            for (uint32_t j = 0; j < c; ++j) {          /* the first SER_D, then the spill */
                 uint32_t sl = h + j;
                 sl = sl >= SR ? sl - SR : sl;
-                if (j < c) m.st(S_RG + (uint32_t)SER_D * nd + j, b[(12u + sl) * NP]);
+                const uint32_t e = b[(12u + sl) * NP];
+                if (j < (uint32_t)SER_D) m.st(S_RG + (uint32_t)SER_D * nd + j, e);
+                else m.sp_st(nd, j - (uint32_t)SER_D, e);
+            }
+            if (c > (uint32_t)SER_D) {
+                s_byte_set(r.sc0, r.sc1, nd, c - (uint32_t)SER_D);
+                r.spl |= 1u << nd;
             }
             r.cnt |= (c < (uint32_t)SER_D ? c : (uint32_t)SER_D) << (4u * nd);
             r.nz |= (c ? 1u : 0u) << nd;
@@ -1102,7 +1111,6 @@ ser_kernel(const SimArgs *Ap) {
         r.A = r.nz | r.iss;
         tn = 0xFFu;
         nxv = pfv = false;
-        if (deep) return SR_OVF;
         if (r.A == 0u) {
             r.st = (r.dmp == NPM) ? SS_COMPLETED : SS_DEADLOCKED;
             return SR_DONE;
@@ -1137,9 +1145,13 @@ ser_kernel(const SimArgs *Ap) {
                 tci = c;
             }
         }
+        /* word (ip & 7) / 2 of cur by masks: a select chain on a run-time index is turned
+         * into a stack copy and an indexed scratch load */
         const uint32_t j = ip & 7u;
-        const uint32_t wd = (j & 4u) ? ((j & 2u) ? cur.w : cur.z) : ((j & 2u) ? cur.y : cur.x);
-        return (j & 1u) ? (wd >> 16) : (wd & 0xFFFFu);
+        const uint32_t m2 = 0u - ((j >> 1) & 1u), m4 = 0u - ((j >> 2) & 1u);
+        const uint32_t lo = (cur.x & ~m2) | (cur.y & m2), hi = (cur.z & ~m2) | (cur.w & m2);
+        const uint32_t wd = (lo & ~m4) | (hi & m4);
+        return (wd >> (16u * (j & 1u))) & 0xFFFFu;
     };
     auto refill = [&]() {
         /* pf (chunk pfc, issued at an earlier refill) becomes nx once cur reaches pfc - 1;
@@ -1490,7 +1502,7 @@ extern "C" void dsm_close(dsm_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *ptrs[] = {c->d_ctrl, c->d_args, c->d_ovf_list, c->d_susp, c->d_susp_list,
+    void *ptrs[] = {c->d_ctrl, c->d_args, c->d_ovf_list, c->d_susp, c->d_susp_list, c->d_spill,
                     c->d_traces, c->d_counts,
                     c->d_res, c->d_cnt, c->d_recs, c->d_table, c->d_issue, c->d_issue_n};
     for (void *p : ptrs) if (p) (void)hipFree(p);
@@ -1580,6 +1592,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
         if ((rc = ensure(&c->d_susp_list, &c->susp_list_cap, (size_t)n_sys))) return rc;
     }
     if ((rc = ensure(&c->d_recs, &c->recs_cap, (size_t)n_sys * np * 8))) return rc;
+    if (use_ser && (rc = ensure(&c->d_spill, &c->spill_cap, (size_t)c->cus * 64 * SER_WAVES * 8 * 256))) return rc;
     if (!d_results) {   /* the engine needs the per-system header even if the caller does not */
         if ((rc = ensure(&c->d_res, &c->res_cap, (size_t)n_sys + 1))) return rc;
         d_results = c->d_res;
@@ -1623,6 +1636,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.susp_list = c->d_susp_list;
     A.susp_count = c->d_ctrl + CTRL_SUSP;
     A.susp_ring = (uint32_t)ring_eff;
+    A.spill = c->d_spill;
     if (tr) {
         A.issue = c->d_issue;
         A.issue_n = c->d_issue_n;

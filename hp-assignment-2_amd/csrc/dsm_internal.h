@@ -28,6 +28,8 @@ struct dsm_ctx {
     size_t susp_cap;
     uint32_t *d_susp_list;           /*   and the suspended system ids                       */
     size_t susp_list_cap;
+    uint32_t *d_spill;               /* serial resume: per-lane inbox spill FIFOs            */
+    size_t spill_cap;
     uint16_t *d_traces;
     size_t traces_cap;
     uint32_t *d_counts;

@@ -25,10 +25,13 @@
  * A round in which no node has an action ends the system (`rounds` counts the active ones).
  *
  * Inboxes are D-deep FIFOs here (the analysis in DESIGN.md: after round 2^12 a C3 inbox
- * holds at most 2 messages at any moment in 99.9% of systems).  An append to a full FIFO
- * ends the system's run here with SR_OVF: the caller hands the system to the 256-deep
- * re-run from scratch, as the lock-step kernel does with its ring overflows, so results never
- * depend on D.
+ * holds at most 2 messages at any moment in 99.9% of systems), continued in a per-node
+ * spill FIFO (global memory on the device) when they fill: entries past the first D are
+ * appended to the spill and move into the FIFO's tail as its head is popped, so the order is
+ * the inbox's.  An inbox that would exceed the inbox limit `cap` (MSG_BUFFER_SIZE, :12, or
+ * dsm_set_inbox_limit) ends the system's run here with SR_OVF: the caller hands the system
+ * to the 256-deep re-run from scratch, which reports RING_OVERFLOW exactly (the count here
+ * can be one higher than at the end of the round, so that hand-off is conservative).
  */
 #ifndef DSM_SERIAL_H
 #define DSM_SERIAL_H
@@ -68,6 +71,9 @@ struct SReg {
     uint32_t msgs;    /* messages handled                                                   */
     uint32_t asrt;    /* an assert fired in this round                                      */
     uint32_t st;      /* status once SR_DONE                                                */
+    uint32_t spl;     /* nodes whose inbox continues in the spill                           */
+    uint32_t sc0, sc1;   /* spill counts, a byte per node (nodes 0-3, 4-7)                  */
+    uint32_t sh0, sh1;   /* spill heads, a byte per node (a 256-entry ring per node)        */
 };
 
 DSM_HD uint32_t s_nib(uint32_t w, uint32_t n) { return (w >> (4u * n)) & 15u; }
@@ -77,6 +83,18 @@ DSM_HD uint32_t s_set2(uint32_t w, uint32_t i, uint32_t v) {
     return (w & ~(3u << sh)) | (v << sh);
 }
 DSM_HD uint32_t s_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
+/* byte n of the 8-byte value (hi:lo) -- two registers, not an array (an array indexed at
+ * run time goes to scratch memory) */
+DSM_HD uint32_t s_byte(uint32_t lo, uint32_t hi, uint32_t n) {
+    return (((n & 4u) ? hi : lo) >> (8u * (n & 3u))) & 0xFFu;
+}
+DSM_HD void s_byte_set(uint32_t &lo, uint32_t &hi, uint32_t n, uint32_t v) {
+    const uint32_t sh = 8u * (n & 3u);
+    const uint32_t w = (n & 4u) ? hi : lo;
+    const uint32_t x = (w & ~(0xFFu << sh)) | (v << sh);
+    lo = (n & 4u) ? lo : x;
+    hi = (n & 4u) ? x : hi;
+}
 
 /* a fresh system: initializeProcessor :778-790 and main :142-146 for every node */
 template <int NP, class M>
@@ -92,6 +110,7 @@ DSM_HD void ser_fresh(M &m, SReg &r, const uint32_t *counts, uint32_t stride) {
     r.A = r.iss = (1u << NP) - 1u;
     r.E = r.nz = r.dmp = r.cnt = r.head = 0;
     r.rounds = r.msgs = r.asrt = r.st = 0;
+    r.spl = r.sc0 = r.sc1 = r.sh0 = r.sh1 = 0;
 }
 
 /* one node-action of the system (the lowest node left in this round), then, if it was the
@@ -100,11 +119,13 @@ DSM_HD void ser_fresh(M &m, SReg &r, const uint32_t *counts, uint32_t stride) {
  * different system, and divergent branches cost more than the predicated work.
  *   F fetch(node, index, issue) -> the packed instruction (only used when issue);
  *   R on_dump(node): the node's dump record is due (state as stored, flags 2).
- * An append that would make an inbox hold more than cap (<= D) messages ends the run with
- * SR_OVF.  A disabled append writes the scratch word S_RG + 8D. */
+ * M: the system's words (ld / st / ld16 / st16) and its spill FIFOs (sp_ld / sp_st (node,
+ * index), 256 entries per node).  An append that would make an inbox hold more than cap
+ * (<= 256) messages ends the run with SR_OVF.  A disabled append writes the scratch word
+ * S_RG + 8D. */
 template <int NP, int D, class M, class T, class F, class R>
 DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, uint32_t lim_rsh,
-                         uint32_t cap = (uint32_t)D) {
+                         uint32_t cap = 256u) {
     constexpr uint32_t NPM = (1u << NP) - 1u, SCR = S_RG + 8u * (uint32_t)D;
     const uint32_t n = s_ctz(r.A), n4 = 4u * n, bit = 1u << n;
     uint32_t ct = m.ld(S_CT + n);
@@ -121,8 +142,18 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
         const uint32_t nh = (r.head & ~(15u << n4)) | (hn << n4);
         r.head = hasMsg ? nh : r.head;
         r.cnt -= hasMsg ? (1u << n4) : 0u;
-        r.nz &= (hasMsg && s_nib(r.cnt, n) == 0u) ? ~bit : ~0u;
+        r.nz &= (hasMsg && s_nib(r.cnt, n) == 0u && !(r.spl & bit)) ? ~bit : ~0u;
         r.msgs += hasMsg ? 1u : 0u;
+        if (hasMsg && (r.spl & bit)) {       /* the spill's head moves to the FIFO's tail */
+            const uint32_t scn = s_byte(r.sc0, r.sc1, n), shn = s_byte(r.sh0, r.sh1, n);
+            uint32_t slot = hn + s_nib(r.cnt, n);
+            slot = slot >= (uint32_t)D ? slot - (uint32_t)D : slot;
+            m.st(S_RG + (uint32_t)D * n + slot, m.sp_ld(n, shn));
+            r.cnt += 1u << n4;
+            s_byte_set(r.sh0, r.sh1, n, (shn + 1u) & 0xFFu);
+            s_byte_set(r.sc0, r.sc1, n, scn - 1u);
+            r.spl &= scn > 1u ? ~0u : ~bit;
+        }
     }
     ct += doIssue ? (1u << 16) : 0u;
     const uint32_t op = doDump ? (uint32_t)DT_DUMP : dt_type(w);
@@ -162,13 +193,22 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
     bool ovf = false;
     auto append = [&](bool en, uint32_t d, uint32_t e) {
         const uint32_t c = s_nib(r.cnt, d);
-        const bool ok = en && c < cap;
-        ovf = ovf || (en && c >= cap);
+        const bool sp = (r.spl >> d) & 1u;
+        const uint32_t scd = sp ? s_byte(r.sc0, r.sc1, d) : 0u;
+        const bool over = en && c + scd >= cap;
+        const bool fifo = en && !over && !sp && c < (uint32_t)D;
+        const bool spill = en && !over && !fifo;
+        ovf = ovf || over;
         uint32_t slot = s_nib(r.head, d) + c;
         slot = slot >= (uint32_t)D ? slot - (uint32_t)D : slot;
-        m.st(ok ? S_RG + (uint32_t)D * d + slot : SCR, e);
-        r.cnt += ok ? 1u << (4u * d) : 0u;
-        r.nz |= ok ? 1u << d : 0u;
+        m.st(fifo ? S_RG + (uint32_t)D * d + slot : SCR, e);
+        r.cnt += fifo ? 1u << (4u * d) : 0u;
+        r.nz |= en && !over ? 1u << d : 0u;
+        if (spill) {                          /* the FIFO is full: continue in the spill */
+            m.sp_st(d, (s_byte(r.sh0, r.sh1, d) + scd) & 0xFFu, e);
+            s_byte_set(r.sc0, r.sc1, d, scd + 1u);
+            r.spl |= 1u << d;
+        }
     };
     {
         uint32_t dm = o.o0 >> 24;

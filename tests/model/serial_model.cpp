@@ -3,11 +3,12 @@
  * (hp-assignment-2_amd/csrc/dsm_serial.h, the resume-pass kernel's per-lane engine) run on
  * the host over whole systems from their first round, against the oracle
  * (oracle/dsm_oracle.c): per-system status, rounds, messages, instructions, and the dump and
- * final records of every node (as their hashes).  Systems whose inbox would exceed the
- * D-deep FIFO end with SR_OVF (the kernel hands them to the 256-deep re-run); they are
- * counted, not compared.
+ * final records of every node (as their hashes).  Inboxes deeper than the D-deep FIFO
+ * continue in the spill (counted as "spilled"); systems whose inbox would exceed the inbox
+ * limit end with SR_OVF (the kernel hands them to the 256-deep re-run, which reports
+ * RING_OVERFLOW); they are counted, not compared.
  *
- *   serial_model <np> <dist> <n_sys> <D> <round_limit_log2 (0 = default)> <instr>
+ *   serial_model <np> <dist> <n_sys> <D> <round_limit_log2 (0 = default)> <instr> [inbox cap]
  *   (dist 3: 8-node uniform addresses on a 4-node system, so instructions whose home is
  *   not simulated raise the defined ASSERT_FAILED deviation)
  *   -> JSON {"systems", "compared", "ovf", "by_status": [...]}; exit 1 on the first mismatch
@@ -26,10 +27,13 @@ namespace {
 
 struct HostCol {
     uint32_t *p;
+    uint32_t *spill;                     /* [node][256] */
     uint32_t ld(uint32_t w) const { return p[w]; }
     void st(uint32_t w, uint32_t v) const { p[w] = v; }
     uint32_t ld16(uint32_t w, uint32_t h) const { return reinterpret_cast<const uint16_t *>(&p[w])[h]; }
     void st16(uint32_t w, uint32_t h, uint32_t v) const { reinterpret_cast<uint16_t *>(&p[w])[h] = (uint16_t)v; }
+    uint32_t sp_ld(uint32_t d, uint32_t i) const { return spill[d * 256 + i]; }
+    void sp_st(uint32_t d, uint32_t i, uint32_t v) const { spill[d * 256 + i] = v; }
 };
 struct HostTab {
     const uint32_t *t;
@@ -45,7 +49,7 @@ void to_rec(HostCol &m, uint32_t n, uint32_t flags, dsm_rec *out) {
 }
 
 template <int NP, int D>
-int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr) {
+int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t cap) {
     static uint32_t tab[DT_TABLE_WORDS];
     if (dt_build(tab) > DT_ENTRIES) return 2;
     const HostTab T{tab};
@@ -67,13 +71,14 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr) {
     std::vector<dsm_res> ores(n_sys);
     std::vector<dsm_rec> odump((size_t)n_sys * NP), ofin((size_t)n_sys * NP);
     if (lim_log2) orc_set_round_limit(1u << lim_log2);
-    orc_run_packed(NP, traces.data(), counts.data(), stride, n_sys, 256, ores.data(), odump.data(),
+    orc_run_packed(NP, traces.data(), counts.data(), stride, n_sys, cap, ores.data(), odump.data(),
                    ofin.data(), nullptr, 8);
     const uint32_t lim = lim_log2 ? lim_log2 : 22;
     uint64_t compared = 0, ovf = 0, by_status[5] = {0, 0, 0, 0, 0};
-    std::vector<uint32_t> col(dsms::s_words(D));
+    std::vector<uint32_t> col(dsms::s_words(D)), spill(8 * 256);
+    uint64_t spilled = 0;
     for (uint64_t s = 0; s < n_sys; ++s) {
-        HostCol m{col.data()};
+        HostCol m{col.data(), spill.data()};
         dsms::SReg r;
         const uint16_t *tr = traces.data() + s * NP * stride;
         dsms::ser_fresh<NP>(m, r, counts.data() + s * NP, stride);
@@ -82,9 +87,12 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr) {
         auto fetch = [&](uint32_t n, uint32_t i, bool iss) -> uint32_t { return iss ? tr[(size_t)n * stride + i] : 0u; };
         auto on_dump = [&](uint32_t n) { to_rec(m, n, 2u, &dump[n]); };
         uint32_t v;
+        bool sp = false;
         do {
-            v = dsms::ser_step<NP, D>(m, r, T, fetch, on_dump, lim);
+            v = dsms::ser_step<NP, D>(m, r, T, fetch, on_dump, lim, cap);
+            sp = sp || r.spl;
         } while (v == dsms::SR_RUN);
+        spilled += sp;
         if (v == dsms::SR_OVF) { ++ovf; continue; }
         dsm_res mine;
         mine.status = r.st | (r.dmp << 8);
@@ -119,8 +127,9 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr) {
         ++compared;
         ++by_status[r.st];
     }
-    printf("{\"systems\": %llu, \"compared\": %llu, \"ovf\": %llu, \"by_status\": [%llu, %llu, %llu, %llu, %llu]}\n",
+    printf("{\"systems\": %llu, \"compared\": %llu, \"ovf\": %llu, \"spilled\": %llu, \"by_status\": [%llu, %llu, %llu, %llu, %llu]}\n",
            (unsigned long long)n_sys, (unsigned long long)compared, (unsigned long long)ovf,
+           (unsigned long long)spilled,
            (unsigned long long)by_status[0], (unsigned long long)by_status[1],
            (unsigned long long)by_status[2], (unsigned long long)by_status[3],
            (unsigned long long)by_status[4]);
@@ -131,13 +140,14 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr) {
 
 int main(int argc, char **argv) {
     if (argc < 7) return 2;
-    const int np = atoi(argv[1]), dist = atoi(argv[2]), D = atoi(argv[5 - 1]);
+    const int np = atoi(argv[1]), dist = atoi(argv[2]), D = atoi(argv[4]);
     const uint64_t n = strtoull(argv[3], nullptr, 10);
     const uint32_t lim = (uint32_t)atoi(argv[5]), ni = (uint32_t)atoi(argv[6]);
-    if (np == 8 && D == 4) return run<8, 4>(dist, n, lim, ni);
-    if (np == 8 && D == 2) return run<8, 2>(dist, n, lim, ni);
-    if (np == 8 && D == 8) return run<8, 8>(dist, n, lim, ni);
-    if (np == 4 && D == 4) return run<4, 4>(dist, n, lim, ni);
-    if (np == 4 && D == 8) return run<4, 8>(dist, n, lim, ni);
+    const uint32_t cap = argc > 7 ? (uint32_t)atoi(argv[7]) : 256u;
+    if (np == 8 && D == 4) return run<8, 4>(dist, n, lim, ni, cap);
+    if (np == 8 && D == 2) return run<8, 2>(dist, n, lim, ni, cap);
+    if (np == 8 && D == 8) return run<8, 8>(dist, n, lim, ni, cap);
+    if (np == 4 && D == 4) return run<4, 4>(dist, n, lim, ni, cap);
+    if (np == 4 && D == 2) return run<4, 2>(dist, n, lim, ni, cap);
     return 2;
 }

@@ -2,7 +2,8 @@
 
 The budget pass (lock-step, 8 lanes per system) suspends every system still running after
 2^budget rounds; ser_kernel continues each on ONE lane, one node-action per iteration, with
-the inboxes as 4-deep FIFOs (deeper ones hand the system to the 256-deep re-run from scratch).
+the inboxes as 4-deep FIFOs continued in per-lane spill FIFOs in HBM (only an inbox beyond the
+inbox limit hands the system to the 256-deep re-run from scratch).
 It must be exact: per-system results, dump and final records, and counters equal the oracle's
 single pass, and equal the lock-step resume pass (DSM_SERIAL=0), at budgets that suspend
 systems early (inboxes still busy, many hand-offs) and late (the C3 tail), and for the
@@ -68,6 +69,8 @@ def test_serial_resume_vs_oracle(dsm, orc, monkeypatch, np_, dist, ring, blog):
             if (mask >> nd) & 1:
                 assert np.array_equal(d, odump[s, nd]), (s, nd)
     assert cnt["resumed"] > 0 and info["budget_log2"] == blog
+    if ring >= 12:          # deep inboxes spill instead of going to the 256-deep re-run
+        assert cnt["overflow_reruns"] == 0
     assert cnt["systems"] == n and cnt["msgs"] == int(ores["msgs"].sum())
     assert cnt["instrs"] == int(ores["instrs"].sum()) and cnt["rounds"] == int(ores["rounds"].sum())
     assert cnt["sum_final_hash"] == int(ores["final_hash"].sum(dtype=np.uint64))
@@ -109,8 +112,9 @@ def test_serial_round_limit(dsm, orc, monkeypatch, limit_log2, blog):
 
 @pytest.mark.parametrize("cap", [2, 3, 6])
 def test_serial_inbox_limit(dsm, orc, monkeypatch, cap):
-    """An inbox limit below, at and above the serial FIFO depth (4): deeper inboxes go to the
-    256-deep re-run, which reports RING_OVERFLOW exactly."""
+    """An inbox limit below, at and above the serial FIFO depth (4): inboxes deeper than the
+    FIFO continue in the spill, those that would pass the limit go to the 256-deep re-run,
+    which reports RING_OVERFLOW exactly."""
     n = 4096
     tr, cn = orc.generate(8, "uniform", 13, 4096, 0, n)
     ores, _ = orc.run_packed(8, tr, cn, ring_cap=cap, nthreads=16)[:2]
