@@ -70,6 +70,7 @@ struct SimArgs {
     /* two-pass schedule (run_engine): a budget pass suspends every system still running
      * after 1 << rsh rounds, a resume pass continues them from their saved state */
     uint32_t rsh;                   /* round-limit test: rounds >> rsh != 0                  */
+    uint32_t rsh_ff;                /* the same for a kernel with the hit-run fast-forward    */
     uint32_t budget;                /* budget pass: suspend at 1 << rsh rounds               */
     uint32_t resume;                /* resume pass: start() restores a suspended system      */
     uint32_t ffsel;                 /* one of a fast-forward / plain pair of launches: run only
@@ -421,7 +422,8 @@ sim_kernel(const SimArgs *Ap) {
     /* an inbox beyond ocap ends the round's system: the fast kernel hands it to the 256-deep
      * re-run (its ring holds RING), which reports RING_OVERFLOW beyond the inbox limit */
     const uint32_t ocap = FB || (LIM && Ap->icap < (uint32_t)RING) ? Ap->icap : (uint32_t)RING;
-    uint32_t rsh = BUD && Ap->rsh < lim_rsh ? Ap->rsh : lim_rsh;   /* wave-uniform (an SGPR) */
+    const uint32_t arsh = FF ? Ap->rsh_ff : Ap->rsh;
+    uint32_t rsh = BUD && arsh < lim_rsh ? arsh : lim_rsh;   /* wave-uniform (an SGPR) */
     const uint32_t late_rsh = BUD ? Ap->late_rsh : 0u;
     const bool budget = BUD && Ap->budget != 0, resume = BUD && Ap->resume != 0;
     /* systems started statically (one per slot), the rest claimed from the shard counters.
@@ -1630,6 +1632,10 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.lim_rsh = c->round_limit_log2;
     A.icap = c->inbox_limit;
     A.rsh = blog ? blog : RSH_MAX;
+    /* hit-run workloads (the fast-forward kernel) run their systems ~2^12 rounds in all: a
+     * budget of 2^12 would suspend almost every one just before its end (measured on C4:
+     * 2^12 / 2^13 / 2^14 -> 63.3 / 61.5 / 61.5 ms) */
+    A.rsh_ff = blog ? (blog + 1 < RSH_MAX ? blog + 1 : RSH_MAX) : RSH_MAX;
     A.budget = blog ? 1u : 0u;
     A.late_rsh = (blog && c->late_log2 > 0 && c->late_log2 < blog) ? c->late_log2 : 0u;
     A.susp = c->d_susp;
@@ -1650,7 +1656,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     B.claim = c->d_ctrl + CTRL_FB;
     B.ovf_list = nullptr;
     B.ovf_count = nullptr;
-    B.rsh = RSH_MAX;
+    B.rsh = B.rsh_ff = RSH_MAX;
     B.budget = 0;
     SimArgs &C = pk.a[2];           /* resume pass: the suspended list, count on the device */
     C = A;
@@ -1658,7 +1664,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     C.d_n = c->d_ctrl + CTRL_SUSP;
     C.list = c->d_susp_list;
     C.claim = c->d_ctrl + CTRL_RES;
-    C.rsh = RSH_MAX;
+    C.rsh = C.rsh_ff = RSH_MAX;
     C.budget = 0;
     C.late_rsh = 0;
     C.resume = 1;

@@ -198,7 +198,9 @@ def test_two_pass_schedule(dsm, orc, monkeypatch, dist, ring, blog):
                     assert np.array_equal(d, odump[s, nd])
     _cmp(res, ores)
     assert info["budget_log2"] == blog
-    longer = int((ores["rounds"] >= (1 << blog)).sum())
+    # hit-run traces take the fast-forward kernel, whose budget is one doubling longer
+    eff = blog + 1 if dist == "hot" else blog
+    longer = int((ores["rounds"] >= (1 << eff)).sum())
     assert cnt["resumed"] >= longer - cnt["overflow_reruns"] and cnt["resumed"] > 0
     assert info["resume_blocks"] > 0
     assert cnt["systems"] == n and cnt["msgs"] == int(ores["msgs"].sum())
