@@ -16,8 +16,8 @@ import os
 import sys
 
 d, config = sys.argv[1], sys.argv[2]
-KERNELS = {"sim_kernel": "::sim_kernel<", "gen_kernel": "::gen_kernel<", "parse_kernel": "::parse_kernel<",
-           "fmt_kernel": "::fmt_kernel<"}
+KERNELS = {"sim_kernel": "::sim_kernel<", "ser_kernel": "::ser_kernel<", "gen_kernel": "::gen_kernel<",
+           "parse_kernel": "::parse_kernel<", "fmt_kernel": "::fmt_kernel<"}
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(d, "pmc_fetch", "*counter_collection.csv")) + \
         glob.glob(os.path.join(d, "pmc_write", "*counter_collection.csv")):
@@ -31,7 +31,7 @@ for k, v in vals.items():
     per = collections.defaultdict(list)
     for (cname, _disp), xs in v.items():
         per[cname].append(sum(xs) * 1024.0)       # KB -> bytes, summed over the dispatch's rows
-    if k == "sim_kernel":
+    if k in ("sim_kernel", "ser_kernel"):
         # the packed path launches a fast-forward / plain pair per pass and one of the two
         # exits at once (ffscan_kernel's verdict): average over the dispatches that ran
         per = {c: [x for x in xs if x >= (1 << 20)] or xs for c, xs in per.items()}
