@@ -1146,6 +1146,9 @@ ser_kernel(const SimArgs *Ap) {
                 tn = nd;
                 tci = c;
             }
+            /* wait here, in the rare branch: left to the first use after the join, the wait
+             * (vmcnt(0)) lands on the main path and also waits for the refill's prefetches */
+            __builtin_amdgcn_s_waitcnt(0x0F70);             /* vmcnt(0) */
         }
         /* word (ip & 7) / 2 of cur by masks: a select chain on a run-time index is turned
          * into a stack copy and an indexed scratch load */
