@@ -1428,8 +1428,11 @@ static_assert(sizeof(SimArgsPack) % 4 == 0, "SimArgsPack words");
  * (their state to HBM); the resume pass continues those (almost all long, of similar
  * remaining length), sizing its own grid from the device-resident count.  Results are
  * identical: a system's rounds run in the same order, only split across two launches.
- * Defaults: budget 2^12, late budget 2^10; dsm_set_budget (or DSM_BUDGET_LOG2 /
- * DSM_LATE_LOG2 in the environment at dsm_open) change them; budget 0 = one pass. */
+ * With the serial resume pass (ser_kernel) the budget is 2^10 (C3: 2^10 / 2^12 equal, the
+ * tail systems of either budget land 4.5 / 2.3 to a lane; C5: 89.9 vs 101.8 ms), the
+ * fast-forward kernel's 2^9; late budget 2^9 (off at a budget <= 2^9).  dsm_set_budget
+ * (or DSM_BUDGET_LOG2 / DSM_LATE_LOG2 / DSM_FF_BUDGET_LOG2 in the environment at dsm_open)
+ * change them; budget 0 = one pass. */
 static uint32_t env_u32(const char *name, uint32_t dflt) {
     const char *e = getenv(name);
     if (!e || !*e) return dflt;
@@ -1468,9 +1471,11 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->ring = ring;
     c->cus = prop.multiProcessorCount;
     /* tuning knobs: read here once, reported by dsm_launch_info_get */
-    c->budget_log2 = env_u32("DSM_BUDGET_LOG2", 12);
+    c->budget_log2 = env_u32("DSM_BUDGET_LOG2", 10);
     if (c->budget_log2 >= RSH_MAX) c->budget_log2 = 0;
-    c->late_log2 = env_u32("DSM_LATE_LOG2", 10);
+    c->ff_budget_log2 = env_u32("DSM_FF_BUDGET_LOG2", 9);      /* 0: the plain budget */
+    if (c->ff_budget_log2 >= RSH_MAX) c->ff_budget_log2 = 0;
+    c->late_log2 = env_u32("DSM_LATE_LOG2", 9);
     c->round_limit_log2 = RSH_MAX;
     c->inbox_limit = FB_RING;
     c->ff_mode = DSM_FF_AUTO;
@@ -1635,10 +1640,13 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.lim_rsh = c->round_limit_log2;
     A.icap = c->inbox_limit;
     A.rsh = blog ? blog : RSH_MAX;
-    /* hit-run workloads (the fast-forward kernel) run their systems ~2^12 rounds in all: a
-     * budget of 2^12 would suspend almost every one just before its end (measured on C4:
-     * 2^12 / 2^13 / 2^14 -> 63.3 / 61.5 / 61.5 ms) */
-    A.rsh_ff = blog ? (blog + 1 < RSH_MAX ? blog + 1 : RSH_MAX) : RSH_MAX;
+    /* the fast-forward kernel's own budget.  A short one suspends every system of a hit-run
+     * workload at the same round: each pass then holds the systems of a wave in the same
+     * phase, so the groups enter and leave fast-forward mode together and the normal round
+     * is skipped more often (measured on C4, budget 2^8 / 2^9 / 2^10 / 2^11 / 2^13:
+     * 50.9 / 49.1 / 53.4 / 57.7 / 61.3 ms).  Bench mode only: with a round or inbox limit
+     * (M_LIM) the kernel always has the fast-forward step and takes the plain budget. */
+    A.rsh_ff = !blog ? RSH_MAX : (mode == 0 && c->ff_budget_log2) ? c->ff_budget_log2 : blog;
     A.budget = blog ? 1u : 0u;
     A.late_rsh = (blog && c->late_log2 > 0 && c->late_log2 < blog) ? c->late_log2 : 0u;
     A.susp = c->d_susp;

@@ -183,6 +183,7 @@ def test_two_pass_schedule(dsm, orc, monkeypatch, dist, ring, blog):
     half consumed); results, records and counters must equal the oracle's single pass, and
     overflow re-runs (ring 4) must compose with suspension."""
     monkeypatch.setenv("DSM_BUDGET_LOG2", str(blog))
+    monkeypatch.setenv("DSM_FF_BUDGET_LOG2", str(blog))     # the fast-forward kernel's too
     n = 4096
     tr, cn = orc.generate(8, dist, 21, 4096, 777, n)
     with dsm.Engine(8, 4096, ring_cap=ring, snapshots=True) as eng:
@@ -198,9 +199,7 @@ def test_two_pass_schedule(dsm, orc, monkeypatch, dist, ring, blog):
                     assert np.array_equal(d, odump[s, nd])
     _cmp(res, ores)
     assert info["budget_log2"] == blog
-    # hit-run traces take the fast-forward kernel, whose budget is one doubling longer
-    eff = blog + 1 if dist == "hot" else blog
-    longer = int((ores["rounds"] >= (1 << eff)).sum())
+    longer = int((ores["rounds"] >= (1 << blog)).sum())
     assert cnt["resumed"] >= longer - cnt["overflow_reruns"] and cnt["resumed"] > 0
     assert info["resume_blocks"] > 0
     assert cnt["systems"] == n and cnt["msgs"] == int(ores["msgs"].sum())
