@@ -70,7 +70,6 @@ struct SimArgs {
     /* two-pass schedule (run_engine): a budget pass suspends every system still running
      * after 1 << rsh rounds, a resume pass continues them from their saved state */
     uint32_t rsh;                   /* round-limit test: rounds >> rsh != 0                  */
-    uint32_t rsh_ff;                /* the same for a kernel with the hit-run fast-forward    */
     uint32_t budget;                /* budget pass: suspend at 1 << rsh rounds               */
     uint32_t resume;                /* resume pass: start() restores a suspended system      */
     uint32_t ffsel;                 /* one of a fast-forward / plain pair of launches: run only
@@ -86,6 +85,8 @@ struct SimArgs {
                                      * dsm_set_inbox_limit): RING_OVERFLOW beyond it        */
     uint32_t susp_ring;             /* resume pass: ring depth of the suspended states       */
     uint32_t *spill;                /* serial resume: [lane][node][256] inbox spill FIFOs    */
+    uint32_t thr_ff;                /* budget pass, fast-forward kernel: suspend at this many
+                                     * rounds (0: at 1 << rsh)                               */
 };
 /* the argument blocks of one run, written to device memory by args_kernel (stream-ordered:
  * no pinned staging whose reuse would need a host wait) */
@@ -422,8 +423,10 @@ sim_kernel(const SimArgs *Ap) {
     /* an inbox beyond ocap ends the round's system: the fast kernel hands it to the 256-deep
      * re-run (its ring holds RING), which reports RING_OVERFLOW beyond the inbox limit */
     const uint32_t ocap = FB || (LIM && Ap->icap < (uint32_t)RING) ? Ap->icap : (uint32_t)RING;
-    const uint32_t arsh = FF ? Ap->rsh_ff : Ap->rsh;
-    uint32_t rsh = BUD && arsh < lim_rsh ? arsh : lim_rsh;   /* wave-uniform (an SGPR) */
+    const uint32_t rsh0 = BUD && Ap->rsh < lim_rsh ? Ap->rsh : lim_rsh;
+    /* the round test's threshold: the round limit, or the budget pass's budget (wave-uniform) */
+    uint32_t thr = 1u << rsh0;
+    if (FF && BUD && Ap->budget && Ap->thr_ff && Ap->thr_ff < (1u << lim_rsh)) thr = Ap->thr_ff;
     const uint32_t late_rsh = BUD ? Ap->late_rsh : 0u;
     const bool budget = BUD && Ap->budget != 0, resume = BUD && Ap->resume != 0;
     /* systems started statically (one per slot), the rest claimed from the shard counters.
@@ -792,8 +795,8 @@ sim_kernel(const SimArgs *Ap) {
             uint32_t opv = op;
             asm volatile("" : "+v"(opv));
             const uint64_t actb = __ballot(opv != OP_IDLE || stall) | (WFF ? ffm : 0ull);
-            /* rounds >> rsh: the round limit, or the budget pass's 1 << rsh */
-            const uint64_t flagb = __ballot(((nd.ctl & C_ASSERT) | (rounds >> rsh)) != 0u) |
+            /* rounds >= thr: the round limit, or the budget pass's budget */
+            const uint64_t flagb = __ballot((nd.ctl & C_ASSERT) != 0u || rounds >= thr) |
                                    __ballot(nccv > ocap);
             constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
             constexpr uint64_t GHI = GLO << (NP - 1);
@@ -804,8 +807,8 @@ sim_kernel(const SimArgs *Ap) {
             const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
             const bool gbad = ((badb >> gbase) & NPM) != 0;
             if (gact == 0) --rounds;
-            /* budget pass: a system still running after 1 << rsh rounds is suspended */
-            const bool susp = budget && gact != 0 && !gbad && rounds >= (1u << rsh) && (rounds >> lim_rsh) == 0u;
+            /* budget pass: a system still running after thr rounds is suspended */
+            const bool susp = budget && gact != 0 && !gbad && rounds >= thr && (rounds >> lim_rsh) == 0u;
             const bool done = live && (gact == 0 || gbad || (rounds >> lim_rsh) != 0u || susp);
 
             const uint64_t doneb = __ballot(done);
@@ -901,7 +904,7 @@ sim_kernel(const SimArgs *Ap) {
             /* budget pass: once a slot of this wave found no new system, the wave's remaining
              * systems get the late budget, so the launch's tail is not a system claimed last
              * running its full budget at falling occupancy (the resume pass continues them) */
-            if (budget && late_rsh && (liveb & ~nlive)) rsh = late_rsh < rsh ? late_rsh : rsh;
+            if (budget && late_rsh && (liveb & ~nlive) && (1u << late_rsh) < thr) thr = 1u << late_rsh;
             liveb = nlive;
     };
 
@@ -1473,8 +1476,13 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     /* tuning knobs: read here once, reported by dsm_launch_info_get */
     c->budget_log2 = env_u32("DSM_BUDGET_LOG2", 10);
     if (c->budget_log2 >= RSH_MAX) c->budget_log2 = 0;
-    c->ff_budget_log2 = env_u32("DSM_FF_BUDGET_LOG2", 9);      /* 0: the plain budget */
+    /* the fast-forward kernel's budget in rounds (0: the plain budget); DSM_FF_BUDGET_LOG2,
+     * if set, gives it as a power of two */
+    c->ff_budget_log2 = env_u32("DSM_FF_BUDGET_LOG2", 0);
     if (c->ff_budget_log2 >= RSH_MAX) c->ff_budget_log2 = 0;
+    c->ff_budget_rounds = getenv("DSM_FF_BUDGET_LOG2") ? (c->ff_budget_log2 ? 1u << c->ff_budget_log2 : 0u)
+                                                       : env_u32("DSM_FF_BUDGET_ROUNDS", 384);
+    if (c->ff_budget_rounds >= (1u << RSH_MAX)) c->ff_budget_rounds = 0;
     c->late_log2 = env_u32("DSM_LATE_LOG2", 9);
     c->round_limit_log2 = RSH_MAX;
     c->inbox_limit = FB_RING;
@@ -1640,14 +1648,15 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.lim_rsh = c->round_limit_log2;
     A.icap = c->inbox_limit;
     A.rsh = blog ? blog : RSH_MAX;
-    /* the fast-forward kernel's own budget.  A short one suspends every system of a hit-run
-     * workload at the same round: each pass then holds the systems of a wave in the same
-     * phase, so the groups enter and leave fast-forward mode together and the normal round
-     * is skipped more often (measured on C4, budget 2^8 / 2^9 / 2^10 / 2^11 / 2^13:
-     * 50.9 / 49.1 / 53.4 / 57.7 / 61.3 ms).  Bench mode only: with a round or inbox limit
-     * (M_LIM) the kernel always has the fast-forward step and takes the plain budget. */
-    A.rsh_ff = !blog ? RSH_MAX : (mode == 0 && c->ff_budget_log2) ? c->ff_budget_log2 : blog;
+    /* the fast-forward kernel's own budget (thr_ff rounds).  A short one suspends every
+     * system of a hit-run workload at the same round: each pass then holds the systems of a
+     * wave in the same phase, so the groups enter and leave fast-forward mode together and
+     * the normal round is skipped more often (measured on C4, budget 256 / 320 / 384 / 416 /
+     * 512 / 640 / 1024 / 2048 rounds: 50.9 / 48.7 / 48.3 / 48.4 / 49.0 / 50.0 / 53.4 /
+     * 57.7 ms).  Bench mode only: with a round or inbox limit (M_LIM) the kernel always has
+     * the fast-forward step and takes the plain budget. */
     A.budget = blog ? 1u : 0u;
+    A.thr_ff = (mode == 0) ? c->ff_budget_rounds : 0u;
     A.late_rsh = (blog && c->late_log2 > 0 && c->late_log2 < blog) ? c->late_log2 : 0u;
     A.susp = c->d_susp;
     A.susp_list = c->d_susp_list;
@@ -1667,7 +1676,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     B.claim = c->d_ctrl + CTRL_FB;
     B.ovf_list = nullptr;
     B.ovf_count = nullptr;
-    B.rsh = B.rsh_ff = RSH_MAX;
+    B.rsh = RSH_MAX;
     B.budget = 0;
     SimArgs &C = pk.a[2];           /* resume pass: the suspended list, count on the device */
     C = A;
@@ -1675,7 +1684,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     C.d_n = c->d_ctrl + CTRL_SUSP;
     C.list = c->d_susp_list;
     C.claim = c->d_ctrl + CTRL_RES;
-    C.rsh = C.rsh_ff = RSH_MAX;
+    C.rsh = RSH_MAX;
     C.budget = 0;
     C.late_rsh = 0;
     C.resume = 1;

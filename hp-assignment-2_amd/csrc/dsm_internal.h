@@ -50,6 +50,7 @@ struct dsm_ctx {
      * DSM_BUDGET_LOG2 / DSM_LATE_LOG2, read once at dsm_open) */
     uint32_t budget_log2, late_log2, round_limit_log2, inbox_limit;
     uint32_t ff_budget_log2;         /* the fast-forward kernel's budget (DSM_FF_BUDGET_LOG2) */
+    uint32_t ff_budget_rounds;       /* ... as a round count, any value (DSM_FF_BUDGET_ROUNDS) */
     int ff_mode;                       /* DSM_FF_OFF / ON / AUTO */
     int serial;                        /* resume pass in serial form (ser_kernel; DSM_SERIAL) */
     /* dsm_text.hip tuning (DSM_FMT / DSM_PARSE_BPL, read once at dsm_open) */

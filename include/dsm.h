@@ -249,7 +249,8 @@ int dsm_kernel_ms_history(dsm_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);
  * lane (DSM_SERIAL=0 at dsm_open: the lock-step resume), or, for traces the fast-forward
  * verdict picks, the fast-forward lock-step kernel with its own budget.
  * Results never depend on it.  Defaults 10 / 9 (or DSM_BUDGET_LOG2 / DSM_LATE_LOG2 at
- * dsm_open); the fast-forward kernel's budget is 2^9 (DSM_FF_BUDGET_LOG2). */
+ * dsm_open); the fast-forward kernel's budget is 384 rounds (DSM_FF_BUDGET_ROUNDS, or
+ * DSM_FF_BUDGET_LOG2 as a power of two; 0 = the plain budget). */
 int dsm_set_budget(dsm_ctx *ctx, uint32_t budget_log2, uint32_t late_log2);
 /* Round limit of the following runs: a system still active after 1 << limit_log2 rounds
  * stops with DSM_ROUND_LIMIT (1 <= limit_log2 <= 22; 0 = DSM_MAX_ROUNDS). */
