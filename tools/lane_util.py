@@ -13,4 +13,4 @@ with pydsm.Engine(8, 4096, timing=True) as eng:
         eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
         torch.cuda.synchronize()
         c = pydsm.counters_to_dict(cnt.cpu().numpy().view(np.uint64))
-        print(sys.argv[1], eng.last_kernel_ms(), "wave_rounds", c["wave_rounds"], "live lane-iters", c["ff_passes"], "resumed", c["resumed"])
+        print(sys.argv[1], eng.last_kernel_ms(), "wave_rounds", c["wave_rounds"], "ff_passes", c["ff_passes"], "ff_steps", c["ff_steps"], "resumed", c["resumed"])
