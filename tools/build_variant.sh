@@ -6,7 +6,7 @@ set -e
 NAME=$1; shift
 T=$(mktemp -d)
 cp -r hp-assignment-2_amd/csrc include "$T/"
-for e in "$@"; do sed -i "$e" "$T/csrc/dsm_engine.hip"; done
+for e in "$@"; do sed -i "$e" "$T/csrc/${FILE:-dsm_engine.hip}"; done
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$T/include ${EXTRA:-}"
 $H -c "$T/csrc/dsm_engine.hip" -o "$T/e.o" 2>"$T/warn.txt" || { cat "$T/warn.txt"; exit 1; }
 grep -i "spill\|occupancy" "$T/warn.txt" | head -5 || true
