@@ -239,6 +239,36 @@ def test_full_size_1m_random(dsm, orc):
     _cmp(res[999_000:1_000_024], golden_ensemble("np8_uniform_far"))
 
 
+@pytest.mark.parametrize("dist,n", [("hot", 1 << 20), ("evict", 1 << 21)])
+def test_full_size_c4_c5(dsm, orc, dist, n):
+    """C4 (1M hot-line systems: the fast-forward kernel in both passes, every system
+    suspended at its 384-round budget) and C5 (2M eviction-heavy systems: budget pass + serial
+    resume) at full size, traces resident in HBM: per-system results and the aggregate
+    counters equal the oracle over every system."""
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+    with dsm.Engine(8, 4096) as eng:
+        tr = torch.empty((n, 8, 4096), dtype=torch.int16, device="cuda")
+        cn = torch.empty((n, 8), dtype=torch.int32, device="cuda")
+        out = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(32, dtype=torch.int64, device="cuda")
+        eng.generate_device(dist, 1, 4096, 0, n, tr.data_ptr(), cn.data_ptr(), st)
+        eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
+        torch.cuda.synchronize()
+        res = out.cpu().numpy().view(dsm.RESULT_DTYPE).reshape(-1)
+        cd = dsm.counters_to_dict(cnt.cpu().numpy().view(np.uint64))
+        del tr, cn
+        torch.cuda.empty_cache()
+    assert cd["resumed"] > 0
+    ores, _ = orc.run_generated(8, dist, 1, 4096, 0, n, nthreads=16)
+    _cmp(res, ores)
+    assert cd["systems"] == n and cd["max_rounds"] == int(ores["rounds"].max())
+    assert cd["sum_final_hash"] == int(ores["final_hash"].sum(dtype=np.uint64))
+    assert cd["sum_dump_hash"] == int(ores["dump_hash"].sum(dtype=np.uint64))
+    assert cd["msgs"] == int(ores["msgs"].sum()) and cd["instrs"] == int(ores["instrs"].sum())
+    assert cd["rounds"] == int(ores["rounds"].sum())
+
+
 def test_cli_end_to_end(dsm, tmp_path):
     os.symlink(os.path.join(GOLD, "inputs"), tmp_path / "tests")
     for test in TESTS:
