@@ -376,11 +376,16 @@ def main():
         serial = launches == 2 and not ff_picked and os.environ.get("DSM_SERIAL", "1") != "0"
         roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
-                    kernel=("sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel with the hit-run fast-forward"
-                            if ff_picked else "sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain")
-                           + "; 4-wave groups, ring 12, packed traces; picked per run by ffscan_kernel's trace sample)"
-                           + (f"; budget pass (2^{li['budget_log2']} rounds) + resume pass" if launches == 2 else "")
-                           + (" in serial form (ser_kernel<8>: one lane per suspended system)" if serial else ""),
+                    kernel=(("sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain) budget pass "
+                             "(the fast-forward budget, 384 rounds by default) + sim_kernel<8, 12, 4, false, 0, 5> resume "
+                             "pass with the hit-run fast-forward; 4-wave groups, ring 12, packed traces; the pair picked per "
+                             "run by ffscan_kernel's trace sample")
+                            if ff_picked and launches == 2 and not args.fused else
+                            ("sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel with the hit-run fast-forward"
+                             if ff_picked else "sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain")
+                            + "; 4-wave groups, ring 12, packed traces; picked per run by ffscan_kernel's trace sample)"
+                            + (f"; budget pass (2^{li['budget_log2']} rounds) + resume pass" if launches == 2 else "")
+                            + (" in serial form (ser_kernel<8>: one lane per suspended system)" if serial else "")),
                     launches_per_step=launches,
                     algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),
                     per_unit="2 B per consumed packed instruction + 32 B result + 4*np B counts per system"
