@@ -247,7 +247,8 @@ int dsm_kernel_ms_history(dsm_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);
  * running after 1 << budget_log2 rounds (0 = one pass), 1 << late_log2 once a wave finds no
  * new system (0 = off); the resume pass continues them -- in serial form, one system per
  * lane (DSM_SERIAL=0 at dsm_open: the lock-step resume), or, for traces the fast-forward
- * verdict picks, the fast-forward lock-step kernel with its own budget.
+ * verdict picks, the fast-forward lock-step kernel (their budget pass: the plain kernel at
+ * the fast-forward budget).
  * Results never depend on it.  Defaults 10 / 9 (or DSM_BUDGET_LOG2 / DSM_LATE_LOG2 at
  * dsm_open); the fast-forward kernel's budget is 384 rounds (DSM_FF_BUDGET_ROUNDS, or
  * DSM_FF_BUDGET_LOG2 as a power of two; 0 = the plain budget). */
