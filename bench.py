@@ -168,6 +168,16 @@ def cpu_baseline_reference(dist, n_instr, seed, n_sample, procs):
                        f"{t:.2f} s (generation and initializeProcessor untimed)")
 
 
+def golden_aggregate(config):
+    """The full-size golden aggregate of a bench workload (oracle/gen_fixtures.py aggregates:
+    the reference's handler text over every system), or None."""
+    try:
+        with open(os.path.join(REPO, "tests", "golden", "aggregates.json")) as f:
+            return json.load(f).get(config)
+    except (OSError, ValueError):
+        return None
+
+
 def traffic_from_profiles(config):
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -402,14 +412,35 @@ def main():
                              (trace_stream, "gen_kernel")):
             if phase is not None and tr.get(kname):
                 phase["traffic"] = tr[kname].get("bytes_per_launch")
+        # parity after the timed region: the last step's per-system results against the
+        # reference's own handler text -- the full-size golden aggregates (counters, status
+        # counts, hash sums, per-system result digest; tests/golden/aggregates.json) and the
+        # golden per-system prefix (tests/golden/ensemble/np8_<dist>.npy)
         parity = None
-        if args.config == "random" and rank == 0 and first == 0 and n_sys >= 4096:
-            g = np.load(os.path.join(REPO, "tests", "golden", "ensemble", "np8_uniform.npy"))
-            r = out[:4096].cpu().numpy().view(pydsm.RESULT_DTYPE).reshape(-1)
-            mine = np.stack([r["status"].astype(np.uint64), r["rounds"].astype(np.uint64),
-                             r["msgs"].astype(np.uint64), r["instrs"].astype(np.uint64),
-                             r["dump_hash"], r["final_hash"]], axis=1)
-            parity = "golden[0:4096] bit-exact" if np.array_equal(mine, g) else "GOLDEN MISMATCH"
+        if rank == 0 and first == 0 and not args.systems:
+            res_host = out.cpu().numpy().view(pydsm.RESULT_DTYPE).reshape(-1)
+            gold = golden_aggregate(args.config)
+            checks = []
+            if gold is not None and gold["systems"] == n_sys:
+                mine = pydsm.aggregate(res_host)
+                diff = pydsm.aggregate_diff(mine, gold)
+                for k in ("msgs", "instrs", "rounds", "systems", "max_rounds"):
+                    if local_c[k] != gold[k] and k not in diff:
+                        diff.append("counter " + k)
+                if local_c["sum_final_hash"] != int(gold["sum_final_hash"], 16):
+                    diff.append("counter sum_final_hash")
+                checks.append("full-size aggregate == reference" if not diff else
+                              "AGGREGATE MISMATCH: " + ",".join(diff))
+            gp = os.path.join(REPO, "tests", "golden", "ensemble", f"np8_{dname}.npy")
+            if os.path.exists(gp):
+                g = np.load(gp)
+                r = res_host[:len(g)]
+                mine = np.stack([r["status"].astype(np.uint64), r["rounds"].astype(np.uint64),
+                                 r["msgs"].astype(np.uint64), r["instrs"].astype(np.uint64),
+                                 r["dump_hash"], r["final_hash"]], axis=1)
+                checks.append(f"golden[0:{len(g)}] bit-exact" if np.array_equal(mine, g)
+                              else "GOLDEN MISMATCH")
+            parity = "; ".join(checks) if checks else None
         cpu = cpu_port = None
         if world == 1 and not args.no_cpu:
             hc = host_cpu()

@@ -306,7 +306,7 @@ class Engine:
                "dsm_kernel_ms_history")
         return [float(x) for x in ms[:n.value]]
 
-    def set_budget(self, budget_log2, late_log2=10):
+    def set_budget(self, budget_log2, late_log2=9):
         _check(lib().dsm_set_budget(self.ctx, budget_log2, late_log2), "dsm_set_budget")
 
     def set_round_limit(self, limit_log2):
@@ -369,3 +369,53 @@ def pack_instr(op, addr, value=0):
     """'R'/'W' + address + value -> packed u16 (bit15 WR, bits 8-14 address, bits 0-7 value)."""
     wr = 1 if op in ("W", "WR") else 0
     return (wr << 15) | ((addr & 0x7F) << 8) | ((value & 0xFF) if wr else 0)
+
+
+# -- full-size aggregates (tests/golden/aggregates.json; oracle/dsm_common.h dsm_result_digest)
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _fmix64(z):
+    z = z ^ (z >> np.uint64(33))
+    z = z * np.uint64(0xff51afd7ed558ccd)
+    z = z ^ (z >> np.uint64(33))
+    z = z * np.uint64(0xc4ceb9fe1a85ec53)
+    return z ^ (z >> np.uint64(33))
+
+
+def result_digest(res, first_idx=0):
+    """Sum mod 2^64 over systems of dsm_result_digest(index, result): position-sensitive, so
+    it pins every system's result, not only the totals.  `res` is a RESULT_DTYPE array."""
+    res = np.ascontiguousarray(res).view(RESULT_DTYPE).reshape(-1)
+    with np.errstate(over="ignore"):
+        idx = np.arange(first_idx, first_idx + len(res), dtype=np.uint64)
+        h = _fmix64(idx * np.uint64(0x9E3779B97F4A7C15) + np.uint64(1))
+        h = _fmix64(h ^ (res["status"].astype(np.uint64) | (res["rounds"].astype(np.uint64) << np.uint64(32))))
+        h = _fmix64(h ^ (res["msgs"].astype(np.uint64) | (res["instrs"].astype(np.uint64) << np.uint64(32))))
+        h = _fmix64(h ^ res["dump_hash"])
+        h = _fmix64(h ^ res["final_hash"])
+        return int(h.sum(dtype=np.uint64))
+
+
+def aggregate(res):
+    """The golden-aggregate view of per-system results (gen_fixtures.py aggregates)."""
+    res = np.ascontiguousarray(res).view(RESULT_DTYPE).reshape(-1)
+    st = np.bincount((res["status"] & 0xFF).astype(np.int64), minlength=5)
+    with np.errstate(over="ignore"):
+        return {"systems": int(len(res)), "msgs": int(res["msgs"].sum(dtype=np.uint64)),
+                "instrs": int(res["instrs"].sum(dtype=np.uint64)),
+                "rounds": int(res["rounds"].sum(dtype=np.uint64)),
+                "max_rounds": int(res["rounds"].max()) if len(res) else 0,
+                "status": [int(x) for x in st[:5]],
+                "sum_dump_hash": "0x%016x" % int(res["dump_hash"].sum(dtype=np.uint64)),
+                "sum_final_hash": "0x%016x" % int(res["final_hash"].sum(dtype=np.uint64)),
+                "result_digest": "0x%016x" % result_digest(res)}
+
+
+AGG_KEYS = ("systems", "msgs", "instrs", "rounds", "max_rounds", "status", "sum_dump_hash",
+            "sum_final_hash", "result_digest")
+
+
+def aggregate_diff(mine, gold):
+    """Keys whose values differ between two aggregate dicts (empty: equal)."""
+    return [k for k in AGG_KEYS if mine.get(k) != gold.get(k)]

@@ -83,6 +83,20 @@ static inline uint64_t dsm_hash_rec(int node, const dsm_rec *r, int nwords) {
 #define DSM_DUMP_WORDS 15
 #define DSM_FINAL_WORDS 16
 
+/* per-system result digest (the full-size golden aggregates, tests/golden/aggregates.json):
+ * summed mod 2^64 over the systems of a workload, idx = the system's index in it.  Sensitive
+ * to every field of every system's result and to its position (bench.py computes it from the
+ * GPU's per-system results, tests/test_aggregates.py pins the numpy restatement). */
+static inline uint64_t dsm_result_digest(uint64_t idx, uint32_t status, uint32_t rounds,
+                                         uint32_t msgs, uint32_t instrs, uint64_t dump_hash,
+                                         uint64_t final_hash) {
+    uint64_t h = dsm_fmix64(idx * 0x9E3779B97F4A7C15ULL + 1u);
+    h = dsm_fmix64(h ^ ((uint64_t)status | ((uint64_t)rounds << 32)));
+    h = dsm_fmix64(h ^ ((uint64_t)msgs | ((uint64_t)instrs << 32)));
+    h = dsm_fmix64(h ^ dump_hash);
+    return dsm_fmix64(h ^ final_hash);
+}
+
 /* Counter-based synthetic trace generator.  Instruction idx of node `node`
  * of system `sys` depends only on (seed, dist, np, sys, node, idx): results are independent
  * of how systems are batched or sharded over GPUs.  One splitmix64 output feeds 4

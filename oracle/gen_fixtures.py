@@ -36,6 +36,12 @@ outputs.  Nothing written here is reference source text.
   tests/golden/dumps/random_recs.npy           4096 seeded random node records (uint8 [n, 64],
                                                every field in its valid range; record k is
                                                node k % 8)
+  tests/golden/aggregates.json                 full-size aggregates of the bench workloads
+                                               (C3 1M uniform, C4 1M hot, C5 2M evict, and
+                                               the 4096-system np8 fixtures): counters,
+                                               status counts, hash sums and the per-system
+                                               result digest (dsm_common.h), from
+                                               oracle/_ref/ref_lockstep_np8 agg
   tests/golden/dumps/random_md5.json           md5 + length of the reference's OWN
                                                printProcessorState text of each of them
                                                (oracle/_ref/ref_lockstep_np8 fmt)
@@ -173,6 +179,40 @@ def ensemble():
         meta[name] = dict(np=np_, dist=dist, seed=seed, n_instr=n_instr, first_sys=first, n_sys=n)
     with open(os.path.join(d, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
+
+
+# name: dist, seed, n_instr, first_sys, n_sys -- bench.py's CONFIGS at N=1 (rank 0's shard),
+# plus the 4096-system fixtures (pins the numpy digest against np8_*.npy)
+AGGREGATES = {
+    "random": (0, 1, 4096, 0, 1 << 20),
+    "hot": (1, 1, 4096, 0, 1 << 20),
+    "evict": (2, 1, 4096, 0, 2 << 20),
+    "np8_uniform": (0, 1, 4096, 0, 4096),
+    "np8_hot": (1, 1, 4096, 0, 2048),
+    "np8_evict": (2, 1, 4096, 0, 4096),
+}
+
+
+def aggregates():
+    """Full-size golden aggregates: the reference's own handler text (ref_lockstep_np8 agg,
+    lock-step schedule) over every system of each bench workload, in forked slices."""
+    p = os.path.join(GOLD, "aggregates.json")
+    out = json.load(open(p)) if os.path.exists(p) else {}
+    only = os.environ.get("AGG_ONLY")
+    for name, (dist, seed, n_instr, first, n) in AGGREGATES.items():
+        if only and name not in only.split(","):
+            continue
+        r = subprocess.run([os.path.join(REFBIN, "ref_lockstep_np8"), "agg", str(dist), str(seed),
+                            str(n_instr), str(first), str(n), str(os.cpu_count() or 8)],
+                           check=True, capture_output=True, text=True)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        d.update(np=8, dist=dist, seed=seed, n_instr=n_instr, first_sys=first,
+                 producer="oracle/_ref/ref_lockstep_np8 agg (assignment.c handler/issue text, "
+                          "lock-step schedule)")
+        out[name] = d
+        print("  ", name, d["msgs"], d["result_digest"], flush=True)
+        with open(p, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
 
 
 EXPLORE_K, EXPLORE_SEED, EXPLORE_THRESH = 256, 7, 0x8000

@@ -26,6 +26,8 @@
  *   ref_lockstep fmt <recs.bin> <out.bin>   (printProcessorState of 64-byte records)
  *   ref_lockstep bench <dist> <seed> <n_instr> <first> <n> <nproc>
  *                                            (CPU baseline: timed run_system, forked slices)
+ *   ref_lockstep agg <dist> <seed> <n_instr> <first> <n> <nproc>
+ *                                            (full-size golden aggregates, forked slices)
  * out.bin: per system one dsm_res, then NUM_PROCS dump records, then NUM_PROCS final records.
  */
 #include <stdio.h>
@@ -226,6 +228,31 @@ static void write_sys(FILE *f, const dsm_res *res, const dsm_rec *dump, const ds
     fwrite(fin, sizeof(dsm_rec), NUM_PROCS, f);
 }
 
+/* full-size golden aggregates (gen_fixtures.py aggregates; bench.py checks the GPU's against
+ * them): sums over systems, status counts, max rounds, and a per-system result digest
+ * (dsm_result_digest, dsm_common.h: position-sensitive, so it pins every system's result,
+ * not only the totals) */
+typedef struct {
+    uint64_t systems, msgs, instrs, rounds, max_rounds, status[5], dh, fh, digest, ns;
+} agg_t;
+
+static void agg_add(agg_t *a, uint64_t idx, const dsm_res *r) {
+    a->systems++;
+    a->msgs += r->msgs; a->instrs += r->instrs; a->rounds += r->rounds;
+    if (r->rounds > a->max_rounds) a->max_rounds = r->rounds;
+    if ((r->status & 0xFFu) < 5u) a->status[r->status & 0xFFu]++;
+    a->dh += r->dump_hash; a->fh += r->final_hash;
+    a->digest += dsm_result_digest(idx, r->status, r->rounds, r->msgs, r->instrs,
+                                   r->dump_hash, r->final_hash);
+}
+
+static void agg_merge(agg_t *a, const agg_t *b) {
+    a->systems += b->systems; a->msgs += b->msgs; a->instrs += b->instrs; a->rounds += b->rounds;
+    if (b->max_rounds > a->max_rounds) a->max_rounds = b->max_rounds;
+    for (int i = 0; i < 5; ++i) a->status[i] += b->status[i];
+    a->dh += b->dh; a->fh += b->fh; a->digest += b->digest;
+}
+
 int main(int argc, char **argv) {
     dsm_res res;
     dsm_rec dump[NUM_PROCS], fin[NUM_PROCS];
@@ -308,12 +335,15 @@ int main(int argc, char **argv) {
         rmdir("tests/empty"); rmdir("tests"); if (chdir("/")) {} rmdir(tmpl);
         return 0;
     }
-    if (argc == 8 && !strcmp(argv[1], "bench")) {
-        /* CPU baseline: the reference's own handler text under the lock-step schedule over
-         * systems first .. first+n-1 of the generator, in nproc forked processes (one slice
-         * each).  Only run_system is timed (CLOCK_MONOTONIC around each call): trace
-         * generation and initializeProcessor's file reads stay outside, as the GPU's timed
-         * region starts with the traces resident in HBM.  Prints one JSON line. */
+    if (argc == 8 && (!strcmp(argv[1], "bench") || !strcmp(argv[1], "agg"))) {
+        /* bench: CPU baseline -- the reference's own handler text under the lock-step
+         * schedule over systems first .. first+n-1 of the generator, in nproc forked
+         * processes (one slice each).  Only run_system is timed (CLOCK_MONOTONIC around each
+         * call): trace generation and initializeProcessor's file reads stay outside, as the
+         * GPU's timed region starts with the traces resident in HBM.
+         * agg: the same run, reported as the full-size golden aggregates (agg_add): counters,
+         * status counts, hash sums and a per-system result digest.  Prints one JSON line. */
+        const int is_agg = !strcmp(argv[1], "agg");
         int dist = atoi(argv[2]);
         uint64_t seed = strtoull(argv[3], 0, 0);
         int n_instr = atoi(argv[4]);
@@ -337,7 +367,8 @@ int main(int argc, char **argv) {
                     FILE *e = fopen(q, "w"); if (e) fclose(e);
                 }
                 if (!freopen("/dev/null", "w", stdout)) _exit(1);
-                uint64_t msgs = 0, instrs = 0, ns = 0;
+                agg_t a;
+                memset(&a, 0, sizeof a);
                 for (uint64_t sy = lo; sy < hi; ++sy) {
                     for (int t = 0; t < NUM_PROCS; ++t) {
                         reset_ctx(t);
@@ -350,39 +381,53 @@ int main(int argc, char **argv) {
                         }
                         C[t].node.instructionCount = n_instr;
                     }
-                    struct timespec a, b;
-                    clock_gettime(CLOCK_MONOTONIC, &a);
+                    struct timespec ta, tb;
+                    clock_gettime(CLOCK_MONOTONIC, &ta);
                     run_system(&res, dump, fin);
-                    clock_gettime(CLOCK_MONOTONIC, &b);
-                    ns += (uint64_t)(b.tv_sec - a.tv_sec) * 1000000000ull + (uint64_t)(b.tv_nsec - a.tv_nsec);
-                    msgs += res.msgs;
-                    instrs += res.instrs;
+                    clock_gettime(CLOCK_MONOTONIC, &tb);
+                    a.ns += (uint64_t)(tb.tv_sec - ta.tv_sec) * 1000000000ull + (uint64_t)(tb.tv_nsec - ta.tv_nsec);
+                    agg_add(&a, sy - first, &res);
                 }
                 for (int t = 0; t < NUM_PROCS; ++t) {
                     char q[64]; snprintf(q, sizeof q, "tests/empty/core_%d.txt", t); unlink(q);
                 }
                 rmdir("tests/empty"); rmdir("tests"); if (chdir("/")) {} rmdir(tmpl);
-                uint64_t outv[3] = {msgs, instrs, ns};
-                if (write(fds[p][1], outv, sizeof outv) != (ssize_t)sizeof outv) _exit(1);
+                if (write(fds[p][1], &a, sizeof a) != (ssize_t)sizeof a) _exit(1);
                 _exit(0);
             }
             close(fds[p][1]);
         }
-        uint64_t msgs = 0, instrs = 0, ns_max = 0, ns_sum = 0;
+        agg_t tot;
+        memset(&tot, 0, sizeof tot);
+        uint64_t ns_max = 0, ns_sum = 0;
         int ok = 1;
         for (int p = 0; p < nproc; ++p) {
-            uint64_t v[3];
-            if (read(fds[p][0], v, sizeof v) != (ssize_t)sizeof v) ok = 0;
-            else { msgs += v[0]; instrs += v[1]; ns_sum += v[2]; if (v[2] > ns_max) ns_max = v[2]; }
+            agg_t v;
+            if (read(fds[p][0], &v, sizeof v) != (ssize_t)sizeof v) ok = 0;
+            else { agg_merge(&tot, &v); ns_sum += v.ns; if (v.ns > ns_max) ns_max = v.ns; }
             close(fds[p][0]);
         }
         int stt;
         while (wait(&stt) > 0) {}
         if (!ok) { fprintf(stderr, "bench: a worker failed\n"); return 1; }
-        printf("{\"msgs\": %llu, \"instrs\": %llu, \"systems\": %llu, \"nproc\": %d, "
-               "\"sim_ns_max\": %llu, \"sim_ns_sum\": %llu}\n",
-               (unsigned long long)msgs, (unsigned long long)instrs, (unsigned long long)n, nproc,
-               (unsigned long long)ns_max, (unsigned long long)ns_sum);
+        if (!is_agg) {
+            printf("{\"msgs\": %llu, \"instrs\": %llu, \"systems\": %llu, \"nproc\": %d, "
+                   "\"sim_ns_max\": %llu, \"sim_ns_sum\": %llu}\n",
+                   (unsigned long long)tot.msgs, (unsigned long long)tot.instrs, (unsigned long long)n, nproc,
+                   (unsigned long long)ns_max, (unsigned long long)ns_sum);
+        } else {
+            printf("{\"systems\": %llu, \"msgs\": %llu, \"instrs\": %llu, \"rounds\": %llu, "
+                   "\"max_rounds\": %llu, \"status\": [%llu, %llu, %llu, %llu, %llu], "
+                   "\"sum_dump_hash\": \"0x%016llx\", \"sum_final_hash\": \"0x%016llx\", "
+                   "\"result_digest\": \"0x%016llx\"}\n",
+                   (unsigned long long)tot.systems, (unsigned long long)tot.msgs,
+                   (unsigned long long)tot.instrs, (unsigned long long)tot.rounds,
+                   (unsigned long long)tot.max_rounds,
+                   (unsigned long long)tot.status[0], (unsigned long long)tot.status[1],
+                   (unsigned long long)tot.status[2], (unsigned long long)tot.status[3],
+                   (unsigned long long)tot.status[4], (unsigned long long)tot.dh,
+                   (unsigned long long)tot.fh, (unsigned long long)tot.digest);
+        }
         return 0;
     }
     if (argc == 4 && !strcmp(argv[1], "fmt")) {

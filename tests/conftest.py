@@ -45,6 +45,12 @@ def ensemble_meta():
         return json.load(f)
 
 
+def golden_aggregate(name):
+    """Full-size aggregates of the reference's handler text (oracle/gen_fixtures.py aggregates)."""
+    with open(os.path.join(GOLD, "aggregates.json")) as f:
+        return json.load(f)[name]
+
+
 def golden_dump(test, core):
     p = os.path.join(GOLD, "lockstep", test, f"core_{core}_output.txt")
     return open(p).read() if os.path.exists(p) else None

@@ -6,7 +6,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import (GOLD, TESTS, golden_dump, golden_ensemble, golden_ensemble_recs,
+from conftest import (GOLD, TESTS, golden_aggregate, golden_dump, golden_ensemble, golden_ensemble_recs,
                       golden_records, inputs_dir, res_to_u64)
 
 pytestmark = pytest.mark.gpu
@@ -237,6 +237,8 @@ def test_full_size_1m_random(dsm, orc):
     # golden prefix / suffix pinned by the reference handler text
     _cmp(res[:4096], golden_ensemble("np8_uniform"))
     _cmp(res[999_000:1_000_024], golden_ensemble("np8_uniform_far"))
+    # full-size aggregates of the reference's handler text (every system, result digest)
+    assert dsm.aggregate_diff(dsm.aggregate(res), golden_aggregate("random")) == []
 
 
 @pytest.mark.parametrize("dist,n", [("hot", 1 << 20), ("evict", 1 << 21)])
@@ -267,6 +269,8 @@ def test_full_size_c4_c5(dsm, orc, dist, n):
     assert cd["sum_dump_hash"] == int(ores["dump_hash"].sum(dtype=np.uint64))
     assert cd["msgs"] == int(ores["msgs"].sum()) and cd["instrs"] == int(ores["instrs"].sum())
     assert cd["rounds"] == int(ores["rounds"].sum())
+    # full-size aggregates of the reference's handler text (every system, result digest)
+    assert dsm.aggregate_diff(dsm.aggregate(res), golden_aggregate(dist)) == []
 
 
 def test_cli_end_to_end(dsm, tmp_path):
