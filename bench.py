@@ -104,15 +104,42 @@ def launch_ranks(n, argv, cmd=None, timeout=None):
     return rc
 
 
+def cgroup_cpus():
+    """CPUs this job may use by its cgroup's CPU quota (cpu.max, cgroup v2; cfs quota, v1),
+    or None when unlimited / unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            return float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        if q > 0:
+            return q / p
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_cpu():
-    """The host's CPU as the baseline uses it: OpenMP threads (OMP_NUM_THREADS, else the
-    CPUs this process may run on), the machine's nproc and the CPU model."""
+    """The host's CPU as the baseline uses it.  The baseline runs on the job's CPU share: the
+    GPU pool gives a one-GPU job 16 CPUs and sets OMP_NUM_THREADS to it (os.cpu_count() shows
+    the whole machine's); the threads used are OMP_NUM_THREADS, else the CPUs this process may
+    run on, capped by the cgroup quota."""
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = os.cpu_count() or 1
     omp = os.environ.get("OMP_NUM_THREADS", "")
+    quota = cgroup_cpus()
     threads = int(omp) if omp.isdigit() and int(omp) > 0 else aff
+    if quota is not None:
+        threads = min(threads, max(1, int(quota)))
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -123,7 +150,7 @@ def host_cpu():
     except OSError:
         pass
     return dict(threads=min(threads, aff), nproc=os.cpu_count(), affinity=aff, model=model,
-                omp_num_threads=omp or None)
+                omp_num_threads=omp or None, cgroup_cpus=quota)
 
 
 def cpu_baseline(dist, n_instr, seed, n_sample, threads):
@@ -454,6 +481,22 @@ def main():
             for b in (cpu, cpu_port):
                 if b is not None:
                     b["host"] = hc
+            # the whole host: the systems are independent and the forked slices share nothing,
+            # so the rate is linear in cores; checked by a second run of the reference leg on
+            # half the processes over half the sample, then scaled to nproc (an estimate: the
+            # pool gives this job a 16-CPU share, measured above)
+            if cpu is not None and cpu["kind"] == "reference" and threads >= 2:
+                half = cpu_baseline_reference(dname, n_instr, seed,
+                                              max(1, min(args.cpu_ref_sample or n_sys, n_sys) // 2),
+                                              threads // 2)
+                if half is not None:
+                    pc, pc_half = cpu["value"] / threads, half["value"] / (threads // 2)
+                    cpu["per_core"] = round(pc, 1)
+                    cpu["linearity"] = dict(cores=threads // 2, per_core=round(pc_half, 1),
+                                            ratio=round(pc / pc_half, 4))
+                    cpu["full_host_estimate"] = dict(
+                        value=round(pc * hc["nproc"], 1), cores=hc["nproc"],
+                        how=f"per-core rate at {threads} processes x nproc (estimate, not measured)")
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": UNIT, "n_gpus": world,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed_max / K * 1e3, 3),

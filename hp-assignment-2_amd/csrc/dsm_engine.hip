@@ -84,7 +84,7 @@ struct SimArgs {
     uint32_t icap;                  /* inbox limit (MSG_BUFFER_SIZE = 256, or
                                      * dsm_set_inbox_limit): RING_OVERFLOW beyond it        */
     uint32_t susp_ring;             /* resume pass: ring depth of the suspended states       */
-    uint32_t *spill;                /* serial resume: [lane][node][256] inbox spill FIFOs    */
+    uint32_t *spill;                /* serial resume: [lane][S_SPILL] queue spill FIFOs      */
     uint32_t thr_ff;                /* budget pass, fast-forward kernel: suspend at this many
                                      * rounds (0: at 1 << rsh)                               */
 };
@@ -994,29 +994,38 @@ sim_kernel(const SimArgs *Ap) {
  * trace while the others wait for good, ~1.3 node-actions per round, so the lock-step
  * kernel's 8 lanes per system would idle ~84% of the time.  The state of 64 systems sits in
  * LDS as one column per lane ([word][lane]: every access is conflict-free and private to
- * its lane, so no barrier or fence is needed); 4 waves of 38 KB fill the CU's 160 KB.  Each
- * lane takes systems from the suspended list (last-suspended first), restores the lock-step
- * state (inboxes into SER_D-deep FIFOs, continued in the lane's spill FIFOs in HBM), runs it
- * to the end and writes its result and final records; only an inbox beyond the inbox limit
- * hands the system to the 256-deep re-run, as a ring overflow of the lock-step kernel does.  The issuing node's trace chunk and the next one are
- * kept in registers (refill step below). */
-constexpr int SER_WAVES = 4, SER_D = 4, SER_RF = 16;
+ * its lane, so no barrier or fence is needed); a system's column is 104 words, so 6 waves
+ * (26 KB each) fill the CU's 160 KB -- two waves on two of the four SIMDs, where round 2's
+ * 153-word column allowed one per SIMD and nothing hid the iteration's dependent chain.
+ * Each lane takes systems from the suspended list (last-suspended first), restores the
+ * lock-step state (every inbox into the system's 8-slot queue, continued in the lane's spill
+ * FIFO in HBM), runs it to the end and writes its result and final records; only an inbox
+ * beyond the inbox limit hands the system to the 256-deep re-run, as a ring overflow of the
+ * lock-step kernel does.  The issuing node's trace chunk and the next one are kept in
+ * registers (refill step below). */
+constexpr int SER_WAVES = 6, SER_RF = 16;
 
-template <int W, int NW>
+template <int W>
 struct LdsCol {
-    uint32_t (&s)[W][NW][64];
+    uint32_t (&s)[W][dsms::S_WORDS][64];
     uint32_t wv, lane;
-    GU32 *sp;                             /* this lane's spill FIFOs, 256 words per node */
+    GU32 *sp;                             /* this lane's spill FIFO, S_SPILL words          */
     DEVI uint32_t ld(uint32_t w) const { return s[wv][w][lane]; }
     DEVI void st(uint32_t w, uint32_t v) const { s[wv][w][lane] = v; }
+    DEVI uint32_t ld8(uint32_t w, uint32_t b) const {
+        return reinterpret_cast<const uint8_t *>(&s[wv][w][lane])[b];
+    }
+    DEVI void st8(uint32_t w, uint32_t b, uint32_t v) const {
+        reinterpret_cast<uint8_t *>(&s[wv][w][lane])[b] = (uint8_t)v;
+    }
     DEVI uint32_t ld16(uint32_t w, uint32_t h) const {
         return reinterpret_cast<const uint16_t *>(&s[wv][w][lane])[h];
     }
     DEVI void st16(uint32_t w, uint32_t h, uint32_t v) const {
         reinterpret_cast<uint16_t *>(&s[wv][w][lane])[h] = (uint16_t)v;
     }
-    DEVI uint32_t sp_ld(uint32_t d, uint32_t i) const { return sp[d * 256u + i]; }
-    DEVI void sp_st(uint32_t d, uint32_t i, uint32_t v) const { sp[d * 256u + i] = v; }
+    DEVI uint32_t sp_ld(uint32_t i) const { return sp[i]; }
+    DEVI void sp_st(uint32_t i, uint32_t v) const { sp[i] = v; }
 };
 struct LdsTab {
     const uint2 (&t)[DT_TABLE_WORDS / 2];
@@ -1029,32 +1038,31 @@ struct LdsTab {
 };
 
 template <int NP>
-__global__ void __launch_bounds__(64 * SER_WAVES) __attribute__((amdgpu_waves_per_eu(1)))
+__global__ void __launch_bounds__(64 * SER_WAVES) __attribute__((amdgpu_waves_per_eu(2)))
 ser_kernel(const SimArgs *Ap) {
     using namespace dsms;
-    constexpr uint32_t NW = s_words(SER_D);
     constexpr uint32_t NPM = (1u << NP) - 1u;
     /* one of a fast-forward / serial pair: the fast-forward lock-step resume takes the run
      * when the trace scan picked fast-forward */
     if (Ap->ffsel && ff_verdict(Ap->scan)) return;
 
-    __shared__ uint32_t s_ser[SER_WAVES][NW][64];
+    __shared__ uint32_t s_ser[SER_WAVES][S_WORDS][64];
     __shared__ uint2 s_tab[DT_TABLE_WORDS / 2];
-    __shared__ unsigned long long s_cnt[SER_WAVES][K_N];
+    __shared__ unsigned long long s_cnt[K_N];          /* the workgroup's counters */
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    if (lane < K_N) s_cnt[wv][lane] = 0;
+    if (threadIdx.x < K_N) s_cnt[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i < DT_TABLE_WORDS / 2; i += 64 * SER_WAVES) s_tab[i] = Ap->table[i];
     __syncthreads();
 
-    const LdsCol<SER_WAVES, NW> m{s_ser, wv, lane,
-                                  (GU32 *)(Ap->spill + ((uint64_t)blockIdx.x * (64 * SER_WAVES) + threadIdx.x) * (8u * 256u))};
+    const LdsCol<SER_WAVES> m{s_ser, wv, lane,
+                              (GU32 *)(Ap->spill + ((uint64_t)blockIdx.x * (64 * SER_WAVES) + threadIdx.x) * S_SPILL)};
     const LdsTab T{s_tab};
     const uint32_t n = *Ap->d_n;
     const uint32_t stride = Ap->stride, lim_rsh = Ap->lim_rsh, SR = Ap->susp_ring;
     const uint32_t cap = Ap->icap;
     const uint16_t *const traces = Ap->traces;
 
-    /* uniform pointers, hoisted (a wave per SIMD leaves registers to spare) */
+    /* uniform pointers, hoisted */
     uint4 *const recs = Ap->recs;
     dsm_sys_result *const results = Ap->results;
     const uint32_t *const list = Ap->list;
@@ -1081,37 +1089,40 @@ ser_kernel(const SimArgs *Ap) {
         sys = list[n - 1 - k];             /* last-suspended first, as the lock-step resume */
         return true;
     };
-    /* the lock-step state the budget pass suspended (sim_kernel's layout [word][node]) */
+    /* the lock-step state the budget pass suspended (sim_kernel's layout [word][node]):
+     * memory / bitVector words as they are, cache lines (addr | value << 8 | state << 16)
+     * split into the address, value and control words, every inbox appended to the queue
+     * (node by node: only each inbox's own order matters) */
     auto start = [&]() -> uint32_t {
         const GU32 *sp = (const GU32 *)(susp + sys * ((uint64_t)susp_words((int)SR) * NP));
-        r.A = r.E = r.nz = r.iss = r.dmp = r.cnt = r.head = 0;
-        r.msgs = r.asrt = r.st = 0;
-        r.spl = r.sc0 = r.sc1 = r.sh0 = r.sh1 = 0;
+        ser_clear(r);
         r.rounds = sp[(12u + SR + 6u) * NP];
         for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {
             const GU32 *b = sp + nd;
 #pragma unroll
             for (uint32_t i = 0; i < 8; ++i) m.st(S_MB + 8u * nd + i, b[i * NP]);
+            uint32_t la = 0, lv = 0, ls = 0;
 #pragma unroll
-            for (uint32_t i = 0; i < 4; ++i) m.st(S_LN + 4u * nd + i, b[(8u + i) * NP]);
+            for (uint32_t i = 0; i < 4; ++i) {
+                const uint32_t l = b[(8u + i) * NP];
+                la |= (l & 0xFFu) << (8 * i);
+                lv |= ((l >> 8) & 0xFFu) << (8 * i);
+                ls |= ((l >> 16) & 3u) << (2 * i);
+            }
+            m.st(S_LA + nd, la);
+            m.st(S_LV + nd, lv);
             const GU32 *q = b + (12u + SR) * NP;
             const uint32_t ctl = q[NP], ip = q[2 * NP], rh = q[4 * NP];
             m.st(S_DS + nd, q[0]);
-            m.st(S_CT + nd, (ctl & 0xFFFFu) | (ip << 16));
-            m.st(S_NI + nd, q[3 * NP]);
+            m.st(S_CT + nd, (ctl & 0x3FFu) | (ls << SC_LS) | (ip << SC_IP));
+            s_set_ni(r, nd, q[3 * NP]);
             const uint32_t h = rh & 0xFFu, c = rh >> 8;
-            for (uint32_t j = 0; j < c; ++j) {          /* the first SER_D, then the spill */
+            for (uint32_t j = 0; j < c; ++j) {
                 uint32_t sl = h + j;
                 sl = sl >= SR ? sl - SR : sl;
-                const uint32_t e = b[(12u + sl) * NP];
-                if (j < (uint32_t)SER_D) m.st(S_RG + (uint32_t)SER_D * nd + j, e);
-                else m.sp_st(nd, j - (uint32_t)SER_D, e);
+                ser_enqueue<S_QN>(m, r, nd, b[(12u + sl) * NP]);   /* <= 8 x 16: fits */
             }
-            if (c > (uint32_t)SER_D) {
-                s_byte_set(r.sc0, r.sc1, nd, c - (uint32_t)SER_D);
-                r.spl |= 1u << nd;
-            }
-            r.cnt |= (c < (uint32_t)SER_D ? c : (uint32_t)SER_D) << (4u * nd);
+            s_byte_add(r.cnt0, r.cnt1, nd, c);
             r.nz |= (c ? 1u : 0u) << nd;
             r.msgs += q[5 * NP] - c;       /* received - still queued = handled */
             r.iss |= ((ctl & (C_WAIT | C_DUMPED)) == 0u ? 1u : 0u) << nd;
@@ -1188,23 +1199,23 @@ ser_kernel(const SimArgs *Ap) {
         if (v == SR_OVF) {               /* to the 256-deep re-run, from scratch */
             const uint32_t pos = atomicAdd(ovf_count, 1u);
             ovf_list[pos] = (uint32_t)sys;
-            atomicAdd(&s_cnt[wv][K_OVFRERUN], 1ull);
+            atomicAdd(&s_cnt[K_OVFRERUN], 1ull);
             return;
         }
         uint32_t ins = 0;
         for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {
-            ins += m.ld(S_CT + nd) >> 16;
+            ins += m.ld(S_CT + nd) >> SC_IP;
             store_rec(nd, ser_final_flags(m, nd), 1u);
         }
         v4u32 res;
         res.x = r.st | (r.dmp << 8); res.y = r.rounds; res.z = r.msgs; res.w = ins;
         ((GV4 *)results)[2 * sys] = res;
-        atomicAdd(&s_cnt[wv][K_MSGS], (unsigned long long)r.msgs);
-        atomicAdd(&s_cnt[wv][K_INSTRS], (unsigned long long)ins);
-        atomicAdd(&s_cnt[wv][K_ROUNDS], (unsigned long long)r.rounds);
-        atomicAdd(&s_cnt[wv][K_SYSTEMS], 1ull);
-        atomicAdd(&s_cnt[wv][K_STATUS + r.st], 1ull);
-        atomicMax(&s_cnt[wv][K_MAXR], (unsigned long long)r.rounds);
+        atomicAdd(&s_cnt[K_MSGS], (unsigned long long)r.msgs);
+        atomicAdd(&s_cnt[K_INSTRS], (unsigned long long)ins);
+        atomicAdd(&s_cnt[K_ROUNDS], (unsigned long long)r.rounds);
+        atomicAdd(&s_cnt[K_SYSTEMS], 1ull);
+        atomicAdd(&s_cnt[K_STATUS + r.st], 1ull);
+        atomicMax(&s_cnt[K_MAXR], (unsigned long long)r.rounds);
     };
 
     bool live = claim();
@@ -1213,7 +1224,7 @@ ser_kernel(const SimArgs *Ap) {
     for (;;) {
 #pragma unroll 1
         for (int k = 0; k < SER_RF; ++k) {
-            if (live && v == SR_RUN) v = ser_step<NP, SER_D>(m, r, T, fetch, on_dump, lim_rsh, cap);
+            if (live && v == SR_RUN) v = ser_step<NP>(m, r, T, fetch, on_dump, lim_rsh, cap);
             if (live && v != SR_RUN) {
                 finish(v);
                 live = claim();
@@ -1224,15 +1235,10 @@ ser_kernel(const SimArgs *Ap) {
         iters += SER_RF;
         if (__ballot(live) == 0) break;
     }
-    if (lane == 0) s_cnt[wv][K_WROUNDS] = iters;
+    if (lane == 0) atomicAdd(&s_cnt[K_WROUNDS], (unsigned long long)iters);
     __syncthreads();
     if (threadIdx.x < K_N) {
-        unsigned long long x = s_cnt[0][threadIdx.x];
-#pragma unroll
-        for (int w = 1; w < SER_WAVES; ++w) {
-            const unsigned long long y = s_cnt[w][threadIdx.x];
-            x = threadIdx.x == K_MAXR ? (y > x ? y : x) : x + y;
-        }
+        const unsigned long long x = s_cnt[threadIdx.x];
         if (x) {
             if (threadIdx.x == K_MAXR) atomicMax(&Ap->counters[K_MAXR], x);
             else atomicAdd(&Ap->counters[threadIdx.x], x);
@@ -1373,9 +1379,10 @@ sim_fn fast_np_gen(int ring, int mode) {
     case 6: return fast_mode<NP, GEN, 6>(ring);
     case 7: return fast_mode<NP, GEN, 7>(ring);
     case M_LIM: return fast_mode<NP, GEN, M_LIM>(ring);
-    case M_NOFF:                        /* packed path only (ffscan_kernel reads traces) */
+    case M_NOFF:                        /* packed path only (ffscan_kernel reads traces); the
+                                         * fused generator has no plain kernel: mode 0 */
         if constexpr (!GEN) return fast_mode<NP, GEN, M_NOFF>(ring);
-        break;
+        else return fast_mode<NP, GEN, 0>(ring);
     default: return fast_mode<NP, GEN, 0>(ring);
     }
 }
@@ -1615,7 +1622,8 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
         if ((rc = ensure(&c->d_susp_list, &c->susp_list_cap, (size_t)n_sys))) return rc;
     }
     if ((rc = ensure(&c->d_recs, &c->recs_cap, (size_t)n_sys * np * 8))) return rc;
-    if (use_ser && (rc = ensure(&c->d_spill, &c->spill_cap, (size_t)c->cus * 64 * SER_WAVES * 8 * 256))) return rc;
+    /* the serial pass's spill FIFOs: S_SPILL words per lane (96 MiB on 256 CUs) */
+    if (use_ser && (rc = ensure(&c->d_spill, &c->spill_cap, (size_t)c->cus * 64 * SER_WAVES * dsms::S_SPILL))) return rc;
     if (!d_results) {   /* the engine needs the per-system header even if the caller does not */
         if ((rc = ensure(&c->d_res, &c->res_cap, (size_t)n_sys + 1))) return rc;
         d_results = c->d_res;

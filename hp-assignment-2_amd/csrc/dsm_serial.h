@@ -24,14 +24,25 @@
  *     empty at the start does not pop what arrived during the round.
  * A round in which no node has an action ends the system (`rounds` counts the active ones).
  *
- * Inboxes are D-deep FIFOs here (the analysis in DESIGN.md: after round 2^12 a C3 inbox
- * holds at most 2 messages at any moment in 99.9% of systems), continued in a per-node
- * spill FIFO (global memory on the device) when they fill: entries past the first D are
- * appended to the spill and move into the FIFO's tail as its head is popped, so the order is
- * the inbox's.  An inbox that would exceed the inbox limit `cap` (MSG_BUFFER_SIZE, :12, or
- * dsm_set_inbox_limit) ends the system's run here with SR_OVF: the caller hands the system
- * to the 256-deep re-run from scratch, which reports RING_OVERFLOW exactly (the count here
- * can be one higher than at the end of the round, so that hand-off is conservative).
+ * Inboxes (round 3): ONE queue per system, not one per node.  After round 2^10 a C3 system
+ * holds at most 3 messages in flight (queued at the round start plus appended during it) in
+ * 98.3% of its rounds and at most 8 in 99.4% of systems ever (tools/analyze_tail.c), so the
+ * system's 8 inboxes share 8 queue slots in append order; byte n of the ownership masks says
+ * which slots hold node n's messages, and node n's head is its first slot in queue order.
+ * Slots are taken at the tail (qh + qn) and freed where popped; the head advances over freed
+ * slots.  When the slot span is full, or anything is already spilled, an append goes to a
+ * per-system spill FIFO (global memory on the device; entries carry their receiver) that
+ * refills the slots in order, so every inbox keeps its order: node n's messages in slots are
+ * older than its spilled ones, and it pops from the spill only when it has none in a slot.
+ * An inbox that would exceed the inbox limit `cap` (MSG_BUFFER_SIZE, :12, or
+ * dsm_set_inbox_limit), 255 messages, or a full spill ends the system's run here with
+ * SR_OVF: the caller hands the system to the 256-deep re-run from scratch, which reports
+ * RING_OVERFLOW exactly (the count here can be one higher than at the end of the round, so
+ * that hand-off is conservative).
+ *
+ * A system's column is 104 words (the per-node queues of round 2 took 33 of its 153): six
+ * 64-lane waves fit one CU's LDS, two waves on two of its SIMDs, against four waves (one per
+ * SIMD) before -- the iteration is a dependent chain that one wave alone cannot hide.
  */
 #ifndef DSM_SERIAL_H
 #define DSM_SERIAL_H
@@ -42,21 +53,25 @@ namespace dsms {
 
 /* per-system words (one LDS column per lane on the device, a plain array on the host):
  *   S_MB + 8n + p   node n, blocks 2p and 2p+1: memory | bitVector << 8 per 16-bit half
- *   S_LN + 4n + i   node n, cache line i: address | value << 8 | state << 16
+ *   S_LA + n        node n, cache line addresses, a byte per line
+ *   S_LV + n        node n, cache line values, a byte per line
  *   S_DS + n        node n, directory states (2 bits per block)
- *   S_CT + n        node n, pendingWriteValue | flags << 8 | instructions issued << 16
- *   S_NI + n        node n, instructions in its trace
- *   S_RG + Dn + j   node n, inbox slot j (ring entries: body | sender << 24)
- *   S_RG + 8D       scratch: the target of a disabled (predicated-off) append          */
-enum : uint32_t { S_MB = 0, S_LN = 64, S_DS = 96, S_CT = 104, S_NI = 112, S_RG = 120 };
-constexpr uint32_t s_words(int D) { return S_RG + 8u * (uint32_t)D + 1u; }   /* + scratch */
+ *   S_CT + n        node n, control: pendingWriteValue 0-7 | wait 8 | dumped 9 |
+ *                   line states 10-17 (2 bits per line) | instructions issued 18-31
+ *   S_Q + s         queue slot s: ring entry (body | sender << 24) | receiver << 27     */
+enum : uint32_t { S_MB = 0, S_LA = 64, S_LV = 72, S_DS = 80, S_CT = 88, S_Q = 96, S_WORDS = 104 };
+constexpr uint32_t S_QN = 8, S_SPILL = 256;      /* queue slots; spill entries per system */
+constexpr uint32_t S_TOMB = 0xFFFFFFFFu;         /* a spill entry taken out of order      */
 
-/* control bits (the lock-step kernel's C_*): wait 8, dumped 9, assert 11 */
-enum : uint32_t { SC_WAIT = DT_CTL_WAIT, SC_DUMPED = 1u << 9, SC_ASSERT = DT_CTL_ASSERT };
+/* control bits (the lock-step kernel's C_*): wait 8, dumped 9; the table's assert bit (11)
+ * is taken out of the control word at once (the system ends at the end of the round) */
+enum : uint32_t { SC_WAIT = DT_CTL_WAIT, SC_DUMPED = 1u << 9, SC_ASSERT = DT_CTL_ASSERT,
+                  SC_LS = 10, SC_IP = 18 };
 enum : uint32_t { SR_RUN = 0, SR_DONE = 1, SR_OVF = 2 };          /* ser_step verdicts */
 /* statuses (include/dsm.h DSM_*) */
 enum : uint32_t { SS_COMPLETED = 0, SS_DEADLOCKED = 1, SS_ASSERT = 3, SS_ROUND_LIMIT = 4 };
-constexpr uint32_t S_LINE_INIT = 0xFFu | (3u << 16);   /* address 0xFF, value 0, INVALID */
+constexpr uint32_t S_LA_INIT = 0xFFFFFFFFu;      /* every line: address 0xFF              */
+constexpr uint32_t S_LS_INIT = 0xFFu << SC_LS;   /* every line INVALID (3)                */
 
 /* a system's registers */
 struct SReg {
@@ -65,97 +80,182 @@ struct SReg {
     uint32_t nz;      /* nodes whose inbox is non-empty now                                 */
     uint32_t iss;     /* nodes neither waiting nor dumped: they issue, or dump, next        */
     uint32_t dmp;     /* nodes that dumped                                                   */
-    uint32_t cnt;     /* inbox counts, a nibble per node                                    */
-    uint32_t head;    /* inbox heads, a nibble per node                                     */
+    uint32_t own0, own1;   /* bit s of byte n: slot s holds a message for node n (0-3, 4-7)   */
+    uint32_t cnt0, cnt1;   /* inbox counts (slots + spill), a byte per node                  */
+    uint32_t L;       /* slots holding a message                                            */
+    uint32_t q;       /* qh 0-2 | qn 3-6 (slots from qh to the tail) | sq 7-15 (spill
+                       * entries, taken ones included) | sh 16-23 (spill head)             */
+    uint32_t ni01, ni23, ni45, ni67;   /* instructions in each node's trace, 16 bits each  */
     uint32_t rounds;  /* active rounds                                                      */
     uint32_t msgs;    /* messages handled                                                   */
     uint32_t asrt;    /* an assert fired in this round                                      */
     uint32_t st;      /* status once SR_DONE                                                */
-    uint32_t spl;     /* nodes whose inbox continues in the spill                           */
-    uint32_t sc0, sc1;   /* spill counts, a byte per node (nodes 0-3, 4-7)                  */
-    uint32_t sh0, sh1;   /* spill heads, a byte per node (a 256-entry ring per node)        */
 };
 
-DSM_HD uint32_t s_nib(uint32_t w, uint32_t n) { return (w >> (4u * n)) & 15u; }
-DSM_HD uint32_t s_get2(uint32_t w, uint32_t i) { return dt_ubfe(w, 2u * i, 2u); }
-DSM_HD uint32_t s_set2(uint32_t w, uint32_t i, uint32_t v) {
-    const uint32_t sh = 2u * i;
-    return (w & ~(3u << sh)) | (v << sh);
-}
 DSM_HD uint32_t s_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
+/* b where bit k of n is set, else a -- by masks (v_bfi): a `?:` of two members of the
+ * register struct is turned into a load from a selected address, which puts the whole
+ * struct in scratch memory */
+DSM_HD uint32_t s_pick(uint32_t a, uint32_t b, uint32_t n, uint32_t k) {
+    const uint32_t m = 0u - ((n >> k) & 1u);
+    return (a & ~m) | (b & m);
+}
 /* byte n of the 8-byte value (hi:lo) -- two registers, not an array (an array indexed at
  * run time goes to scratch memory) */
 DSM_HD uint32_t s_byte(uint32_t lo, uint32_t hi, uint32_t n) {
-    return (((n & 4u) ? hi : lo) >> (8u * (n & 3u))) & 0xFFu;
+    return (s_pick(lo, hi, n, 2) >> (8u * (n & 3u))) & 0xFFu;
 }
-DSM_HD void s_byte_set(uint32_t &lo, uint32_t &hi, uint32_t n, uint32_t v) {
-    const uint32_t sh = 8u * (n & 3u);
-    const uint32_t w = (n & 4u) ? hi : lo;
-    const uint32_t x = (w & ~(0xFFu << sh)) | (v << sh);
-    lo = (n & 4u) ? lo : x;
-    hi = (n & 4u) ? x : hi;
+/* (hi:lo) += x << 8 n (x may be "negative": a wrapped subtraction inside the byte) */
+DSM_HD void s_byte_add(uint32_t &lo, uint32_t &hi, uint32_t n, uint32_t x) {
+    const uint32_t d = x << (8u * (n & 3u));
+    lo += (n & 4u) ? 0u : d;
+    hi += (n & 4u) ? d : 0u;
+}
+DSM_HD uint32_t s_ni(const SReg &r, uint32_t n) {
+    const uint32_t w = s_pick(s_pick(r.ni01, r.ni23, n, 1), s_pick(r.ni45, r.ni67, n, 1), n, 2);
+    return (w >> (16u * (n & 1u))) & 0xFFFFu;
+}
+DSM_HD void s_set_ni(SReg &r, uint32_t n, uint32_t v) {   /* selects: no pointer to a member */
+    const uint32_t sh = 16u * (n & 1u), k = n >> 1;
+    const uint32_t m = ~(0xFFFFu << sh), x = (v & 0xFFFFu) << sh;
+    r.ni01 = k == 0u ? ((r.ni01 & m) | x) : r.ni01;
+    r.ni23 = k == 1u ? ((r.ni23 & m) | x) : r.ni23;
+    r.ni45 = k == 2u ? ((r.ni45 & m) | x) : r.ni45;
+    r.ni67 = k == 3u ? ((r.ni67 & m) | x) : r.ni67;
+}
+DSM_HD uint32_t s_qh(uint32_t q) { return q & 7u; }
+DSM_HD uint32_t s_qn(uint32_t q) { return (q >> 3) & 15u; }
+DSM_HD uint32_t s_sq(uint32_t q) { return (q >> 7) & 511u; }
+DSM_HD uint32_t s_sh(uint32_t q) { return (q >> 16) & 255u; }
+
+/* empty queue, no spill */
+DSM_HD void ser_clear(SReg &r) {
+    r.A = r.E = r.nz = r.iss = r.dmp = 0;
+    r.own0 = r.own1 = r.cnt0 = r.cnt1 = r.L = r.q = 0;
+    r.ni01 = r.ni23 = r.ni45 = r.ni67 = 0;
+    r.rounds = r.msgs = r.asrt = r.st = 0;
+}
+
+/* append entry e (ring entry: body | sender << 24) to node d's inbox, at the queue's tail
+ * or, when the slot span is full or something is already spilled, to the spill.  Returns
+ * false (nothing appended) when the spill is full.  Counts are the caller's. */
+template <uint32_t Q, class M>
+DSM_HD bool ser_enqueue(M &m, SReg &r, uint32_t d, uint32_t e) {
+    const uint32_t qn = s_qn(r.q), sq = s_sq(r.q);
+    if (sq == 0u && qn < Q) {
+        const uint32_t slot = (s_qh(r.q) + qn) & 7u;
+        m.st(S_Q + slot, e | (d << 27));
+        r.L |= 1u << slot;
+        s_byte_add(r.own0, r.own1, d, 1u << slot);
+        r.q += 1u << 3;
+        return true;
+    }
+    if (sq >= S_SPILL) return false;
+    m.sp_st((s_sh(r.q) + sq) & (S_SPILL - 1u), e | (d << 27));
+    r.q += 1u << 7;
+    return true;
+}
+
+/* slow paths (rare: more than 8 messages in flight) ---------------------------------------- */
+/* node n has no message in a slot: its head is its first entry in the spill; take it out
+ * (a tombstone), then drop leading tombstones */
+template <class M>
+DSM_HD uint32_t ser_spill_take(M &m, SReg &r, uint32_t n) {
+    const uint32_t sq = s_sq(r.q), sh = s_sh(r.q);
+    uint32_t e = 0;
+    for (uint32_t i = 0; i < sq; ++i) {
+        const uint32_t ix = (sh + i) & (S_SPILL - 1u);
+        const uint32_t v = m.sp_ld(ix);
+        if (v != S_TOMB && (v >> 27) == n) {
+            e = v;
+            m.sp_st(ix, S_TOMB);
+            break;
+        }
+    }
+    uint32_t h = sh, c = sq;
+    while (c != 0u && m.sp_ld(h) == S_TOMB) { h = (h + 1u) & (S_SPILL - 1u); --c; }
+    r.q = (r.q & 0xFF00007Fu) | (c << 7) | (h << 16);
+    return e;
+}
+/* refill free tail slots from the spill, in order (skipping tombstones) */
+template <uint32_t Q, class M>
+DSM_HD void ser_refill(M &m, SReg &r) {
+    uint32_t qh = s_qh(r.q), qn = s_qn(r.q), sq = s_sq(r.q), sh = s_sh(r.q);
+    while (qn < Q && sq != 0u) {
+        const uint32_t v = m.sp_ld(sh);
+        sh = (sh + 1u) & (S_SPILL - 1u);
+        --sq;
+        if (v == S_TOMB) continue;
+        const uint32_t slot = (qh + qn) & 7u;
+        m.st(S_Q + slot, v);
+        r.L |= 1u << slot;
+        s_byte_add(r.own0, r.own1, v >> 27, 1u << slot);
+        ++qn;
+    }
+    r.q = qh | (qn << 3) | (sq << 7) | (sh << 16);
 }
 
 /* a fresh system: initializeProcessor :778-790 and main :142-146 for every node */
 template <int NP, class M>
 DSM_HD void ser_fresh(M &m, SReg &r, const uint32_t *counts, uint32_t stride) {
+    ser_clear(r);
     for (uint32_t n = 0; n < (uint32_t)NP; ++n) {
         for (uint32_t p = 0; p < 8; ++p)
             m.st(S_MB + 8 * n + p, ((20u * n + 2 * p) & 0xFFu) | (((20u * n + 2 * p + 1) & 0xFFu) << 16));
-        for (uint32_t i = 0; i < 4; ++i) m.st(S_LN + 4 * n + i, S_LINE_INIT);
+        m.st(S_LA + n, S_LA_INIT);
+        m.st(S_LV + n, 0u);
         m.st(S_DS + n, 0xAAAAAAAAu);                       /* every block UNOWNED */
-        m.st(S_CT + n, 0u);
-        m.st(S_NI + n, counts[n] < stride ? counts[n] : stride);
+        m.st(S_CT + n, S_LS_INIT);
+        s_set_ni(r, n, counts[n] < stride ? counts[n] : stride);
     }
     r.A = r.iss = (1u << NP) - 1u;
-    r.E = r.nz = r.dmp = r.cnt = r.head = 0;
-    r.rounds = r.msgs = r.asrt = r.st = 0;
-    r.spl = r.sc0 = r.sc1 = r.sh0 = r.sh1 = 0;
 }
 
 /* one node-action of the system (the lowest node left in this round), then, if it was the
- * round's last, the end of the round.  Branch-free but for the dump record and the rare
- * third-and-later destinations of a multicast: on the device every lane of a wave runs a
- * different system, and divergent branches cost more than the predicated work.
+ * round's last, the end of the round.  Branch-free but for the dump record, the rare third-
+ * and-later destinations of a multicast and the spill paths: on the device every lane of a
+ * wave runs a different system, and divergent branches cost more than the predicated work.
  *   F fetch(node, index, issue) -> the packed instruction (only used when issue);
  *   R on_dump(node): the node's dump record is due (state as stored, flags 2).
- * M: the system's words (ld / st / ld16 / st16) and its spill FIFOs (sp_ld / sp_st (node,
- * index), 256 entries per node).  An append that would make an inbox hold more than cap
- * (<= 256) messages ends the run with SR_OVF.  A disabled append writes the scratch word
- * S_RG + 8D. */
-template <int NP, int D, class M, class T, class F, class R>
+ * M: the system's words (ld / st / ld8 / st8 / ld16 / st16) and its spill FIFO (sp_ld /
+ * sp_st (index), S_SPILL entries).  Q <= 8: the slot span (the kernel's 8; the host model
+ * takes fewer to send more systems through the spill). */
+template <int NP, uint32_t Q = S_QN, class M, class T, class F, class R>
 DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, uint32_t lim_rsh,
                          uint32_t cap = 256u) {
-    constexpr uint32_t NPM = (1u << NP) - 1u, SCR = S_RG + 8u * (uint32_t)D;
-    const uint32_t n = s_ctz(r.A), n4 = 4u * n, bit = 1u << n;
+    constexpr uint32_t NPM = (1u << NP) - 1u;
+    const uint32_t n = s_ctz(r.A), bit = 1u << n;
     uint32_t ct = m.ld(S_CT + n);
-    const uint32_t nins = m.ld(S_NI + n);
-    const uint32_t h0 = s_nib(r.head, n);
-    const uint32_t rw = m.ld(S_RG + (uint32_t)D * n + h0);      /* inbox head (may be stale) */
+    const uint32_t nins = s_ni(r, n);
     const bool hasMsg = (r.E & bit) != 0u;                        /* :158-169 */
-    const bool doIssue = !hasMsg && (ct >> 16) < nins;            /* :590-592 */
+    /* the inbox head: node n's first slot in queue order from qh (k == 8: none; the head is
+     * in the spill) */
+    const uint32_t ob = s_byte(r.own0, r.own1, n);
+    const uint32_t qh = s_qh(r.q);
+    const uint32_t k = s_ctz((((ob | (ob << 8)) >> qh) & 0xFFu) | 0x100u);
+    const uint32_t slot = (qh + k) & 7u;
+    uint32_t rw = m.ld(S_Q + slot);                               /* (may be stale)     */
+    if (hasMsg && k == 8u) rw = ser_spill_take(m, r, n);
+    const uint32_t ip = ct >> SC_IP;
+    const bool doIssue = !hasMsg && ip < nins;                    /* :590-592 */
     const bool doDump = !hasMsg && !doIssue;                      /* :688-697 */
-    const uint32_t ins = fetch(n, ct >> 16, doIssue);
+    const uint32_t ins = fetch(n, ip, doIssue);
     const uint32_t w = hasMsg ? rw : dt_issue_word(ins);
-    {   /* pop the head */
-        const uint32_t hn = (h0 + 1u == (uint32_t)D) ? 0u : h0 + 1u;
-        const uint32_t nh = (r.head & ~(15u << n4)) | (hn << n4);
-        r.head = hasMsg ? nh : r.head;
-        r.cnt -= hasMsg ? (1u << n4) : 0u;
-        r.nz &= (hasMsg && s_nib(r.cnt, n) == 0u && !(r.spl & bit)) ? ~bit : ~0u;
+    {   /* pop the head: free its slot, advance the queue head past free slots */
+        const bool popq = hasMsg && k < 8u;
+        const uint32_t sb = popq ? (1u << slot) : 0u;
+        s_byte_add(r.own0, r.own1, n, 0u - sb);
+        r.L &= ~sb;
+        s_byte_add(r.cnt0, r.cnt1, n, hasMsg ? 0xFFFFFFFFu : 0u);
+        r.nz &= (hasMsg && s_byte(r.cnt0, r.cnt1, n) == 0u) ? ~bit : ~0u;
         r.msgs += hasMsg ? 1u : 0u;
-        if (hasMsg && (r.spl & bit)) {       /* the spill's head moves to the FIFO's tail */
-            const uint32_t scn = s_byte(r.sc0, r.sc1, n), shn = s_byte(r.sh0, r.sh1, n);
-            uint32_t slot = hn + s_nib(r.cnt, n);
-            slot = slot >= (uint32_t)D ? slot - (uint32_t)D : slot;
-            m.st(S_RG + (uint32_t)D * n + slot, m.sp_ld(n, shn));
-            r.cnt += 1u << n4;
-            s_byte_set(r.sh0, r.sh1, n, (shn + 1u) & 0xFFu);
-            s_byte_set(r.sc0, r.sc1, n, scn - 1u);
-            r.spl &= scn > 1u ? ~0u : ~bit;
-        }
+        const uint32_t qn = s_qn(r.q), L = r.L;
+        uint32_t adv = s_ctz((((L | (L << 8)) >> qh) & 0xFFu) | 0x100u);
+        adv = adv < qn ? adv : qn;
+        r.q = (popq && k == 0u) ? ((r.q & ~0x7Fu) | ((qh + adv) & 7u) | ((qn - adv) << 3)) : r.q;
+        if (s_sq(r.q) != 0u && s_qn(r.q) < Q) ser_refill<Q>(m, r);
     }
-    ct += doIssue ? (1u << 16) : 0u;
+    ct += doIssue ? (1u << SC_IP) : 0u;
     const uint32_t op = doDump ? (uint32_t)DT_DUMP : dt_type(w);
 
     /* decode + micro-op table + datapath (dsm_table.h), as in sim_kernel step (2)-(3) */
@@ -164,51 +264,52 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
     const uint32_t blk = in.a & 15u, idx = in.a & 3u;            /* :177-184 */
     const uint32_t mw = S_MB + 8u * n + (blk >> 1);
     const uint32_t mbw = m.ld16(mw, blk & 1u);
-    const uint32_t lw = m.ld(S_LN + 4u * n + idx);
+    const uint32_t La = m.ld8(S_LA + n, idx), Lv = m.ld8(S_LV + n, idx);
     const uint32_t dsw = m.ld(S_DS + n);
+    const uint32_t lsh = SC_LS + 2u * idx;
     in.op = op; in.node = n; in.np_mask = NPM;
-    in.La = lw & 0xFFu; in.Lv = (lw >> 8) & 0xFFu; in.Ls = lw >> 16;
-    in.Db = mbw >> 8; in.Ds = s_get2(dsw, blk); in.Mv = mbw & 0xFFu; in.pend = ct & 0xFFu;
+    in.La = La; in.Lv = Lv; in.Ls = dt_ubfe(ct, lsh, 2u);
+    in.Db = mbw >> 8; in.Ds = dt_ubfe(dsw, 2u * blk, 2u); in.Mv = mbw & 0xFFu; in.pend = ct & 0xFFu;
     uint32_t hix = op | ((in.a >> 4) == n ? 32u : 0u);
     if (NP < 8) hix = (op == DT_RD && (in.a >> 4) >= (uint32_t)NP) ? (uint32_t)DT_ASSERT : hix;
     uint32_t evDb;
     const uint32_t ti = dt_index(in, tab.hdr(hix), &evDb);
     uint32_t W0, W1;
     tab.row(ti, W0, W1);
-    const uint32_t X = dt_perm(lw, w, 0x05040001u) & ~0x80u;
+    const uint32_t X = dt_perm(La | (Lv << 8), w, 0x05040001u) & ~0x80u;   /* {a, v, La, Lv} */
     const uint32_t Y = dt_perm(mbw, ct, 0x0C050400u) | ((evDb & 0xFFu) << 24);
     const DtOut o = dt_apply_xy(in, X, Y, W0, W1, evDb);
-    m.st(S_LN + 4u * n + idx, dt_perm(o.S, o.P, 0x0C040100u));   /* nLa nLv nLs */
-    m.st(S_DS + n, s_set2(dsw, blk, o.nDs));
+    m.st8(S_LA + n, idx, o.P);                                   /* nLa */
+    m.st8(S_LV + n, idx, o.P >> 8);                              /* nLv */
+    m.st(S_DS + n, (dsw & ~(3u << (2u * blk))) | (o.nDs << (2u * blk)));
     m.st16(mw, blk & 1u, o.nMv | (o.nDb << 8));
-    ct = (ct & ~o.cclr) | o.cset | (doDump ? SC_DUMPED : 0u);   /* wait, pending (:633), assert */
+    r.asrt |= o.cset & SC_ASSERT;
+    ct = (ct & ~(o.cclr | (3u << lsh))) | (o.cset & ~SC_ASSERT) | (o.nLs << lsh) |
+         (doDump ? SC_DUMPED : 0u);                              /* wait, pending (:633) */
     m.st(S_CT + n, ct);
     r.dmp |= doDump ? bit : 0u;
     if (doDump) on_dump(n);                  /* printProcessorState(threadId, node), :695 */
     r.iss = (ct & (SC_WAIT | SC_DUMPED)) ? (r.iss & ~bit) : (r.iss | bit);
-    r.asrt |= ct & SC_ASSERT;
 
     /* sendMessage :711-739: the first word to its destinations in ascending order, then the
      * second; each to the tail of the receiver's inbox */
     bool ovf = false;
     auto append = [&](bool en, uint32_t d, uint32_t e) {
-        const uint32_t c = s_nib(r.cnt, d);
-        const bool sp = (r.spl >> d) & 1u;
-        const uint32_t scd = sp ? s_byte(r.sc0, r.sc1, d) : 0u;
-        const bool over = en && c + scd >= cap;
-        const bool fifo = en && !over && !sp && c < (uint32_t)D;
-        const bool spill = en && !over && !fifo;
+        const uint32_t c = s_byte(r.cnt0, r.cnt1, d);
+        const bool over = en && (c >= cap || c >= 255u);
+        const bool ok = en && !over;
+        const uint32_t qn = s_qn(r.q);
+        const bool fast = ok && (r.q & 0xFF80u) == 0u && qn < Q;        /* no spill, a slot */
+        const uint32_t as = (s_qh(r.q) + qn) & 7u;
+        if (fast) m.st(S_Q + as, e | (d << 27));
+        const uint32_t sb = fast ? (1u << as) : 0u;
+        r.L |= sb;
+        s_byte_add(r.own0, r.own1, d, sb);
+        r.q += fast ? (1u << 3) : 0u;
+        s_byte_add(r.cnt0, r.cnt1, d, ok ? 1u : 0u);
+        r.nz |= ok ? 1u << d : 0u;
         ovf = ovf || over;
-        uint32_t slot = s_nib(r.head, d) + c;
-        slot = slot >= (uint32_t)D ? slot - (uint32_t)D : slot;
-        m.st(fifo ? S_RG + (uint32_t)D * d + slot : SCR, e);
-        r.cnt += fifo ? 1u << (4u * d) : 0u;
-        r.nz |= en && !over ? 1u << d : 0u;
-        if (spill) {                          /* the FIFO is full: continue in the spill */
-            m.sp_st(d, (s_byte(r.sh0, r.sh1, d) + scd) & 0xFFu, e);
-            s_byte_set(r.sc0, r.sc1, d, scd + 1u);
-            r.spl |= 1u << d;
-        }
+        if (ok && !fast) ovf = !ser_enqueue<Q>(m, r, d, e) || ovf;  /* the spill (rare)   */
     };
     {
         uint32_t dm = o.o0 >> 24;
@@ -253,15 +354,14 @@ DSM_HD uint32_t ser_rec_word(M &m, uint32_t n, uint32_t flags, int i) {
         const uint32_t e = m.ld(S_DS + n) >> (8 * (i - 8));
         return (e & 3u) | (((e >> 2) & 3u) << 8) | (((e >> 4) & 3u) << 16) | (((e >> 6) & 3u) << 24);
     }
-    if (i < 15) {                       /* cache addresses / values / states */
-        const uint32_t b = (uint32_t)(i - 12);
-        const uint32_t sel = 0x0C0C0400u | (b * 0x00000101u);
-        const uint32_t l0 = m.ld(S_LN + 4u * n), l1 = m.ld(S_LN + 4u * n + 1u);
-        const uint32_t l2 = m.ld(S_LN + 4u * n + 2u), l3 = m.ld(S_LN + 4u * n + 3u);
-        return dt_perm(dt_perm(l3, l2, sel), dt_perm(l1, l0, sel), 0x05040100u);
-    }
+    if (i == 12) return m.ld(S_LA + n);  /* cache addresses */
+    if (i == 13) return m.ld(S_LV + n);  /* cache values    */
     const uint32_t ct = m.ld(S_CT + n);
-    return (ct & 0xFFu) | (flags << 8) | (ct & 0xFFFF0000u);
+    if (i == 14) {                      /* cache states, a byte per line */
+        const uint32_t e = ct >> SC_LS;
+        return (e & 3u) | (((e >> 2) & 3u) << 8) | (((e >> 4) & 3u) << 16) | (((e >> 6) & 3u) << 24);
+    }
+    return (ct & 0xFFu) | (flags << 8) | ((ct >> SC_IP) << 16);
 }
 
 /* record flags of node n at the end: waitingForReply | dumped << 1 */

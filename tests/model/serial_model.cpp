@@ -3,12 +3,13 @@
  * (hp-assignment-2_amd/csrc/dsm_serial.h, the resume-pass kernel's per-lane engine) run on
  * the host over whole systems from their first round, against the oracle
  * (oracle/dsm_oracle.c): per-system status, rounds, messages, instructions, and the dump and
- * final records of every node (as their hashes).  Inboxes deeper than the D-deep FIFO
- * continue in the spill (counted as "spilled"); systems whose inbox would exceed the inbox
- * limit end with SR_OVF (the kernel hands them to the 256-deep re-run, which reports
- * RING_OVERFLOW); they are counted, not compared.
+ * final records of every node (as their hashes).  Systems whose queue outgrows its Q slots
+ * (8 in the kernel; fewer here to exercise it) continue in the spill (counted as
+ * "spilled"); systems whose inbox would exceed the inbox limit end with SR_OVF (the kernel
+ * hands them to the 256-deep re-run, which reports RING_OVERFLOW); they are counted, not
+ * compared.
  *
- *   serial_model <np> <dist> <n_sys> <D> <round_limit_log2 (0 = default)> <instr> [inbox cap]
+ *   serial_model <np> <dist> <n_sys> <Q> <round_limit_log2 (0 = default)> <instr> [inbox cap]
  *   (dist 3: 8-node uniform addresses on a 4-node system, so instructions whose home is
  *   not simulated raise the defined ASSERT_FAILED deviation)
  *   -> JSON {"systems", "compared", "ovf", "by_status": [...]}; exit 1 on the first mismatch
@@ -27,13 +28,15 @@ namespace {
 
 struct HostCol {
     uint32_t *p;
-    uint32_t *spill;                     /* [node][256] */
+    uint32_t *spill;                     /* [S_SPILL] */
     uint32_t ld(uint32_t w) const { return p[w]; }
     void st(uint32_t w, uint32_t v) const { p[w] = v; }
+    uint32_t ld8(uint32_t w, uint32_t b) const { return reinterpret_cast<const uint8_t *>(&p[w])[b]; }
+    void st8(uint32_t w, uint32_t b, uint32_t v) const { reinterpret_cast<uint8_t *>(&p[w])[b] = (uint8_t)v; }
     uint32_t ld16(uint32_t w, uint32_t h) const { return reinterpret_cast<const uint16_t *>(&p[w])[h]; }
     void st16(uint32_t w, uint32_t h, uint32_t v) const { reinterpret_cast<uint16_t *>(&p[w])[h] = (uint16_t)v; }
-    uint32_t sp_ld(uint32_t d, uint32_t i) const { return spill[d * 256 + i]; }
-    void sp_st(uint32_t d, uint32_t i, uint32_t v) const { spill[d * 256 + i] = v; }
+    uint32_t sp_ld(uint32_t i) const { return spill[i]; }
+    void sp_st(uint32_t i, uint32_t v) const { spill[i] = v; }
 };
 struct HostTab {
     const uint32_t *t;
@@ -48,7 +51,7 @@ void to_rec(HostCol &m, uint32_t n, uint32_t flags, dsm_rec *out) {
     memcpy(out, w, 64);
 }
 
-template <int NP, int D>
+template <int NP, uint32_t Q>
 int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t cap) {
     static uint32_t tab[DT_TABLE_WORDS];
     if (dt_build(tab) > DT_ENTRIES) return 2;
@@ -75,7 +78,7 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
                    ofin.data(), nullptr, 8);
     const uint32_t lim = lim_log2 ? lim_log2 : 22;
     uint64_t compared = 0, ovf = 0, by_status[5] = {0, 0, 0, 0, 0};
-    std::vector<uint32_t> col(dsms::s_words(D)), spill(8 * 256);
+    std::vector<uint32_t> col(dsms::S_WORDS), spill(dsms::S_SPILL);
     uint64_t spilled = 0;
     for (uint64_t s = 0; s < n_sys; ++s) {
         HostCol m{col.data(), spill.data()};
@@ -89,8 +92,8 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         uint32_t v;
         bool sp = false;
         do {
-            v = dsms::ser_step<NP, D>(m, r, T, fetch, on_dump, lim, cap);
-            sp = sp || r.spl;
+            v = dsms::ser_step<NP, Q>(m, r, T, fetch, on_dump, lim, cap);
+            sp = sp || dsms::s_sq(r.q) != 0u;
         } while (v == dsms::SR_RUN);
         spilled += sp;
         if (v == dsms::SR_OVF) { ++ovf; continue; }
@@ -101,7 +104,7 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         uint32_t ins = 0;
         uint64_t dh = 0, fh = 0;
         for (uint32_t n = 0; n < (uint32_t)NP; ++n) {
-            ins += m.ld(dsms::S_CT + n) >> 16;
+            ins += m.ld(dsms::S_CT + n) >> dsms::SC_IP;
             dsm_rec f;
             to_rec(m, n, dsms::ser_final_flags(m, n), &f);
             fh += dsm_hash_rec((int)n, &f, DSM_FINAL_WORDS);
@@ -140,14 +143,18 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
 
 int main(int argc, char **argv) {
     if (argc < 7) return 2;
-    const int np = atoi(argv[1]), dist = atoi(argv[2]), D = atoi(argv[4]);
+    const int np = atoi(argv[1]), dist = atoi(argv[2]), D = atoi(argv[4]);   /* D: queue slots Q */
     const uint64_t n = strtoull(argv[3], nullptr, 10);
     const uint32_t lim = (uint32_t)atoi(argv[5]), ni = (uint32_t)atoi(argv[6]);
     const uint32_t cap = argc > 7 ? (uint32_t)atoi(argv[7]) : 256u;
+    if (np == 8 && D == 8) return run<8, 8>(dist, n, lim, ni, cap);
     if (np == 8 && D == 4) return run<8, 4>(dist, n, lim, ni, cap);
     if (np == 8 && D == 2) return run<8, 2>(dist, n, lim, ni, cap);
-    if (np == 8 && D == 8) return run<8, 8>(dist, n, lim, ni, cap);
+    if (np == 8 && D == 1) return run<8, 1>(dist, n, lim, ni, cap);
+    if (np == 4 && D == 8) return run<4, 8>(dist, n, lim, ni, cap);
     if (np == 4 && D == 4) return run<4, 4>(dist, n, lim, ni, cap);
     if (np == 4 && D == 2) return run<4, 2>(dist, n, lim, ni, cap);
+    if (np == 4 && D == 1) return run<4, 1>(dist, n, lim, ni, cap);
+    fprintf(stderr, "serial_model: no build for np %d, Q %d\n", np, D);
     return 2;
 }
