@@ -528,7 +528,57 @@ sim_kernel(const SimArgs *Ap) {
 
     uint32_t wrounds = 0;    /* loop iterations of this wave (uniform) */
     uint64_t ffm = 0;                  /* lanes in fast-forward mode (wave-uniform)          */
+    uint32_t ffip = 0;                 /* FF: the node's instruction index when its group
+                                        * entered fast-forward mode (ff_settle)               */
     uint64_t liveb = __ballot(live);
+    /* hit-run fast-forward, deferred write-back.  While a group is in the mode only the line
+     * tags and states decide its hits (RD: valid; WR: M or E, and a hit on E leaves M, which
+     * is a hit for every later instruction too), so the fast-forward step only counts rounds
+     * and instructions.  What the hits wrote -- each line's value and state M (:640-645) and
+     * pendingWriteValue (:633) -- is applied when the group leaves the mode, before its next
+     * normal round: the last write to each line within [ffip, ip) and the last write overall,
+     * found by scanning the instructions back from ip (all of them hits).  Lanes with go. */
+    auto ff_settle = [&](bool go) {
+        uint32_t need = (go && nd.ip > ffip) ? 0x1Fu : 0u;    /* lines 0-3, pending (bit 4) */
+        uint32_t i = nd.ip, lval = 0, wm = 0, pv = 0;
+        while (__ballot(need != 0u)) {
+            if (need) {
+                const uint32_t c = (i - 1u) >> 3;                  /* chunk of instruction i-1 */
+                uint32_t w[4];
+                if (GEN) {
+                    gen_chunk<NP>(gmul, gdist, gfirst + sys, node, c, w);
+                } else {
+                    const uint4 v = ld16(tb + 8u * c);
+                    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+                }
+#pragma unroll
+                for (int j = 7; j >= 0; --j) {                     /* newest first */
+                    const uint32_t ix = 8u * c + (uint32_t)j;
+                    const uint32_t h = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                    const bool wr = (ix < i) & (ix >= ffip) & ((h & 0x8000u) != 0u);
+                    const uint32_t ln = (h >> 8) & 3u;
+                    const bool tp = wr & ((need & 16u) != 0u), tl = wr & (((need >> ln) & 1u) != 0u);
+                    pv = tp ? (h & 0xFFu) : pv;
+                    const uint32_t sh = 8u * ln;
+                    lval = tl ? ((lval & ~(0xFFu << sh)) | ((h & 0xFFu) << sh)) : lval;
+                    wm |= tl ? (1u << ln) : 0u;
+                    need &= ~((tp ? 16u : 0u) | (tl ? (1u << ln) : 0u));
+                }
+                i = 8u * c;
+                need = i > ffip ? need : 0u;
+            }
+        }
+        if (go && nd.ip > ffip) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((wm >> q) & 1u) {          /* value written, state MODIFIED (0) */
+                    const uint32_t lw = s_line[wv][q][lane];
+                    s_line[wv][q][lane] = (lw & 0xFFu) | (((lval >> (8 * q)) & 0xFFu) << 8);
+                }
+            /* the pending value of the last write (a node that issued no write keeps its own) */
+            nd.ctl = wm ? ((nd.ctl & ~0xFFu) | pv) : nd.ctl;     /* any write also set a line */
+        }
+    };
     /* one lock-step round of every system of the wave; compiled twice: with the
      * fast-forward step and its gating (WFF, while some group of the wave is in
      * fast-forward mode) and without (the plain round the wave runs otherwise) */
@@ -592,27 +642,13 @@ sim_kernel(const SimArgs *Ap) {
                     const bool gany = ((__ballot(iss) >> gbase) & NPM) != 0u;
                     uint32_t r = iss ? run : (dpend || !gany ? 0u : 8u);
                     if (iss && r > nd.nins - nd.ip) r = nd.nins - nd.ip;
-                    /* the round limit: the round that reaches it runs normally */
-                    if (r > (1u << lim_rsh) - 1u - rounds) r = (1u << lim_rsh) - 1u - rounds;
+                    /* the round limit and the budget (thr): the round that reaches it runs
+                     * normally, so a group never finishes or is suspended in the mode */
+                    const uint32_t rmax = rounds + 1u >= thr ? 0u : thr - 1u - rounds;
+                    if (r > rmax) r = rmax;
                     k = gmin<NP>(r);
                     if (iss && k) {
-                        uint32_t lval = 0, wm = 0;
-    #pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            const uint32_t h = (W[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                            if ((uint32_t)j < k && (h & 0x8000u)) {   /* WR hit :633, :640-645 */
-                                const uint32_t sh = (h >> 5) & 0x18u;
-                                lval = (lval & ~(0xFFu << sh)) | ((h & 0xFFu) << sh);
-                                wm |= 1u << (sh >> 3);
-                                nd.ctl = (nd.ctl & ~0xFFu) | (h & 0xFFu);
-                            }
-                        }
-    #pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            if ((wm >> i) & 1u) {   /* value written, state MODIFIED (0) */
-                                const uint32_t lw = s_line[wv][i][lane];
-                                s_line[wv][i][lane] = (lw & 0xFFu) | (((lval >> (8 * i)) & 0xFFu) << 8);
-                            }
+                        /* the write-back of the hits is deferred (ff_settle) */
                         if (!GEN) {     /* consume k from the shift register cur ++ nxt */
                             const bool cross = k >= m;
                             uint32_t X[4];
@@ -631,7 +667,11 @@ sim_kernel(const SimArgs *Ap) {
                 }
                 const uint32_t adv = (uint32_t)__builtin_popcountll(__ballot(inff && node == 0u && k != 0u));
                 if (lane == 0) s_cnt[wv][K_FFPASS] += adv;   /* system steps that advanced */
-                ffm &= ~__ballot(inff && k < 8u);   /* those run this iteration's round normally */
+                /* those leave the mode and run this iteration's round normally, with their
+                 * hits written back first */
+                const uint64_t leave = __ballot(inff && k < 8u);
+                ffm &= ~leave;
+                if (leave) ff_settle(__builtin_amdgcn_inverse_ballot_w64(leave));
             }
             /* still in the mode: no round here (the lane's bit of the wave-uniform mask) */
             const bool inff = WFF && __builtin_amdgcn_inverse_ballot_w64(ffm);
@@ -944,7 +984,9 @@ sim_kernel(const SimArgs *Ap) {
         const uint64_t busy = __ballot(block) | ~liveb;
         const uint64_t nzb = (((busy & FLOW) + FLOW) | busy) & FTOP;
         const uint64_t one = (~nzb & nzh) >> (NP - 1);
-        ffm |= (one << NP) - one;
+        const uint64_t enter = ((one << NP) - one) & ~ffm;
+        ffm |= enter;
+        ffip = __builtin_amdgcn_inverse_ballot_w64(enter) ? nd.ip : ffip;   /* segment start */
         pint = one ? FF_PROBE : (pint < FF_PROBE_MAX ? 2u * pint : FF_PROBE_MAX);
         pcd = pint;
     };
@@ -1008,10 +1050,13 @@ constexpr int SER_WAVES = 6, SER_RF = 16;
 template <int W>
 struct LdsCol {
     uint32_t (&s)[W][dsms::S_WORDS][64];
+    uint32_t *dum;                        /* write-only dummy word of this lane              */
     uint32_t wv, lane;
     GU32 *sp;                             /* this lane's spill FIFO, S_SPILL words          */
     DEVI uint32_t ld(uint32_t w) const { return s[wv][w][lane]; }
     DEVI void st(uint32_t w, uint32_t v) const { s[wv][w][lane] = v; }
+    /* a store when en, else to the dummy word: an address select, not a branch */
+    DEVI void st_if(bool en, uint32_t w, uint32_t v) const { *(en ? &s[wv][w][lane] : dum) = v; }
     DEVI uint32_t ld8(uint32_t w, uint32_t b) const {
         return reinterpret_cast<const uint8_t *>(&s[wv][w][lane])[b];
     }
@@ -1037,7 +1082,7 @@ struct LdsTab {
     }
 };
 
-template <int NP>
+template <int NP, bool CAP>
 __global__ void __launch_bounds__(64 * SER_WAVES) __attribute__((amdgpu_waves_per_eu(2)))
 ser_kernel(const SimArgs *Ap) {
     using namespace dsms;
@@ -1049,12 +1094,13 @@ ser_kernel(const SimArgs *Ap) {
     __shared__ uint32_t s_ser[SER_WAVES][S_WORDS][64];
     __shared__ uint2 s_tab[DT_TABLE_WORDS / 2];
     __shared__ unsigned long long s_cnt[K_N];          /* the workgroup's counters */
+    __shared__ uint32_t s_dum[64];                     /* dummy words (write-only)  */
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     if (threadIdx.x < K_N) s_cnt[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i < DT_TABLE_WORDS / 2; i += 64 * SER_WAVES) s_tab[i] = Ap->table[i];
     __syncthreads();
 
-    const LdsCol<SER_WAVES> m{s_ser, wv, lane,
+    const LdsCol<SER_WAVES> m{s_ser, &s_dum[lane], wv, lane,
                               (GU32 *)(Ap->spill + ((uint64_t)blockIdx.x * (64 * SER_WAVES) + threadIdx.x) * S_SPILL)};
     const LdsTab T{s_tab};
     const uint32_t n = *Ap->d_n;
@@ -1151,12 +1197,14 @@ ser_kernel(const SimArgs *Ap) {
         }
     };
     auto fetch = [&](uint32_t nd, uint32_t ip, bool iss) -> uint32_t {
+        /* bitwise & | on the flags: && / || chains are compiled into branches */
         const uint32_t c = ip >> 3;
-        const bool rot = iss && tn == nd && tci + 1u == c && nxv;        /* next chunk: in nx */
-        const bool miss = iss && !rot && (tn != nd || tci != c);
+        const bool tnd = tn == nd;
+        const bool rot = iss & tnd & (tci + 1u == c) & nxv;              /* next chunk: in nx */
+        const bool miss = iss & !rot & (!tnd | (tci != c));
         cur.x = rot ? nx.x : cur.x; cur.y = rot ? nx.y : cur.y;
         cur.z = rot ? nx.z : cur.z; cur.w = rot ? nx.w : cur.w;
-        nxv = nxv && !rot;
+        nxv = nxv & !rot;
         tci = rot ? c : tci;
         if (__ballot(miss)) {            /* another node issues, or a system's first issue */
             if (miss) {
@@ -1224,7 +1272,7 @@ ser_kernel(const SimArgs *Ap) {
     for (;;) {
 #pragma unroll 1
         for (int k = 0; k < SER_RF; ++k) {
-            if (live && v == SR_RUN) v = ser_step<NP>(m, r, T, fetch, on_dump, lim_rsh, cap);
+            if (live && v == SR_RUN) v = ser_step<NP, S_QN, CAP>(m, r, T, fetch, on_dump, lim_rsh, cap);
             if (live && v != SR_RUN) {
                 finish(v);
                 live = claim();
@@ -1732,7 +1780,11 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
             HIPCK(hipGetLastError());
         }
         if (ser) {
-            hipLaunchKernelGGL(np == 4 ? ser_kernel<4> : ser_kernel<8>, dim3(c->cus), dim3(64 * SER_WAVES), 0, st, a);
+            /* the CAP build keeps per-node inbox counts for an inbox limit below 256 */
+            const bool capb = c->inbox_limit < (uint32_t)FB_RING;
+            hipLaunchKernelGGL(np == 4 ? (capb ? ser_kernel<4, true> : ser_kernel<4, false>)
+                                       : (capb ? ser_kernel<8, true> : ser_kernel<8, false>),
+                               dim3(c->cus), dim3(64 * SER_WAVES), 0, st, a);
             HIPCK(hipGetLastError());
         } else if (pair) {
             hipLaunchKernelGGL(fast_nf, dim3(grid_fast), dim3(64 * FW), 0, st, a);

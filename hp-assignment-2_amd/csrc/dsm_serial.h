@@ -34,11 +34,14 @@
  * per-system spill FIFO (global memory on the device; entries carry their receiver) that
  * refills the slots in order, so every inbox keeps its order: node n's messages in slots are
  * older than its spilled ones, and it pops from the spill only when it has none in a slot.
- * An inbox that would exceed the inbox limit `cap` (MSG_BUFFER_SIZE, :12, or
- * dsm_set_inbox_limit), 255 messages, or a full spill ends the system's run here with
- * SR_OVF: the caller hands the system to the 256-deep re-run from scratch, which reports
- * RING_OVERFLOW exactly (the count here can be one higher than at the end of the round, so
- * that hand-off is conservative).
+ * A system holds at most 8 + S_SPILL_CAP = 256 queued messages (MSG_BUFFER_SIZE, :12): no
+ * inbox can pass the reference's limit, so the default build keeps no per-node counts (an
+ * inbox is non-empty iff its ownership byte is, or its node is in the spill mask).  With an
+ * inbox limit below 256 (dsm_set_inbox_limit; the CAP build) the counts are kept and an
+ * inbox that would exceed the limit, or 255 messages, ends the system's run here with SR_OVF;
+ * so does a full spill in either build: the caller hands the system to the 256-deep re-run
+ * from scratch, which reports RING_OVERFLOW exactly (the count here can be one higher than at
+ * the end of the round, so that hand-off is conservative).
  *
  * A system's column is 104 words (the per-node queues of round 2 took 33 of its 153): six
  * 64-lane waves fit one CU's LDS, two waves on two of its SIMDs, against four waves (one per
@@ -61,6 +64,7 @@ namespace dsms {
  *   S_Q + s         queue slot s: ring entry (body | sender << 24) | receiver << 27     */
 enum : uint32_t { S_MB = 0, S_LA = 64, S_LV = 72, S_DS = 80, S_CT = 88, S_Q = 96, S_WORDS = 104 };
 constexpr uint32_t S_QN = 8, S_SPILL = 256;      /* queue slots; spill entries per system */
+constexpr uint32_t S_SPILL_CAP = 256 - S_QN;     /* used spill entries: 8 + 248 = 256     */
 constexpr uint32_t S_TOMB = 0xFFFFFFFFu;         /* a spill entry taken out of order      */
 
 /* control bits (the lock-step kernel's C_*): wait 8, dumped 9; the table's assert bit (11)
@@ -81,7 +85,8 @@ struct SReg {
     uint32_t iss;     /* nodes neither waiting nor dumped: they issue, or dump, next        */
     uint32_t dmp;     /* nodes that dumped                                                   */
     uint32_t own0, own1;   /* bit s of byte n: slot s holds a message for node n (0-3, 4-7)   */
-    uint32_t cnt0, cnt1;   /* inbox counts (slots + spill), a byte per node                  */
+    uint32_t cnt0, cnt1;   /* CAP build: inbox counts (slots + spill), a byte per node       */
+    uint32_t spl;     /* nodes with a message in the spill                                  */
     uint32_t L;       /* slots holding a message                                            */
     uint32_t q;       /* qh 0-2 | qn 3-6 (slots from qh to the tail) | sq 7-15 (spill
                        * entries, taken ones included) | sh 16-23 (spill head)             */
@@ -131,7 +136,7 @@ DSM_HD uint32_t s_sh(uint32_t q) { return (q >> 16) & 255u; }
 /* empty queue, no spill */
 DSM_HD void ser_clear(SReg &r) {
     r.A = r.E = r.nz = r.iss = r.dmp = 0;
-    r.own0 = r.own1 = r.cnt0 = r.cnt1 = r.L = r.q = 0;
+    r.own0 = r.own1 = r.cnt0 = r.cnt1 = r.spl = r.L = r.q = 0;
     r.ni01 = r.ni23 = r.ni45 = r.ni67 = 0;
     r.rounds = r.msgs = r.asrt = r.st = 0;
 }
@@ -150,13 +155,25 @@ DSM_HD bool ser_enqueue(M &m, SReg &r, uint32_t d, uint32_t e) {
         r.q += 1u << 3;
         return true;
     }
-    if (sq >= S_SPILL) return false;
+    if (sq >= S_SPILL_CAP) return false;
     m.sp_st((s_sh(r.q) + sq) & (S_SPILL - 1u), e | (d << 27));
     r.q += 1u << 7;
+    r.spl |= 1u << d;
     return true;
 }
 
 /* slow paths (rare: more than 8 messages in flight) ---------------------------------------- */
+/* the nodes that still have a message in the spill */
+template <class M>
+DSM_HD uint32_t ser_spill_nodes(M &m, const SReg &r) {
+    const uint32_t sq = s_sq(r.q), sh = s_sh(r.q);
+    uint32_t spl = 0;
+    for (uint32_t i = 0; i < sq; ++i) {
+        const uint32_t v = m.sp_ld((sh + i) & (S_SPILL - 1u));
+        spl |= v != S_TOMB ? 1u << ((v >> 27) & 7u) : 0u;
+    }
+    return spl;
+}
 /* node n has no message in a slot: its head is its first entry in the spill; take it out
  * (a tombstone), then drop leading tombstones */
 template <class M>
@@ -175,6 +192,7 @@ DSM_HD uint32_t ser_spill_take(M &m, SReg &r, uint32_t n) {
     uint32_t h = sh, c = sq;
     while (c != 0u && m.sp_ld(h) == S_TOMB) { h = (h + 1u) & (S_SPILL - 1u); --c; }
     r.q = (r.q & 0xFF00007Fu) | (c << 7) | (h << 16);
+    r.spl = ser_spill_nodes(m, r);
     return e;
 }
 /* refill free tail slots from the spill, in order (skipping tombstones) */
@@ -193,6 +211,7 @@ DSM_HD void ser_refill(M &m, SReg &r) {
         ++qn;
     }
     r.q = qh | (qn << 3) | (sq << 7) | (sh << 16);
+    r.spl = ser_spill_nodes(m, r);
 }
 
 /* a fresh system: initializeProcessor :778-790 and main :142-146 for every node */
@@ -217,10 +236,11 @@ DSM_HD void ser_fresh(M &m, SReg &r, const uint32_t *counts, uint32_t stride) {
  * wave runs a different system, and divergent branches cost more than the predicated work.
  *   F fetch(node, index, issue) -> the packed instruction (only used when issue);
  *   R on_dump(node): the node's dump record is due (state as stored, flags 2).
- * M: the system's words (ld / st / ld8 / st8 / ld16 / st16) and its spill FIFO (sp_ld /
- * sp_st (index), S_SPILL entries).  Q <= 8: the slot span (the kernel's 8; the host model
+ * M: the system's words (ld / st / st_if (a store when the flag is set, else to a dummy
+ * word: no branch) / ld8 / st8 / ld16 / st16) and its spill FIFO (sp_ld / sp_st (index),
+ * S_SPILL entries).  CAP: the build for an inbox limit below 256 (per-node counts kept).  Q <= 8: the slot span (the kernel's 8; the host model
  * takes fewer to send more systems through the spill). */
-template <int NP, uint32_t Q = S_QN, class M, class T, class F, class R>
+template <int NP, uint32_t Q = S_QN, bool CAP = false, class M, class T, class F, class R>
 DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, uint32_t lim_rsh,
                          uint32_t cap = 256u) {
     constexpr uint32_t NPM = (1u << NP) - 1u;
@@ -241,19 +261,22 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
     const bool doDump = !hasMsg && !doIssue;                      /* :688-697 */
     const uint32_t ins = fetch(n, ip, doIssue);
     const uint32_t w = hasMsg ? rw : dt_issue_word(ins);
-    {   /* pop the head: free its slot, advance the queue head past free slots */
-        const bool popq = hasMsg && k < 8u;
+    {   /* pop the head: free its slot, advance the queue head past free slots (branch-free:
+         * bit operations and selects; the head moves only when its own slot was popped) */
+        const bool popq = hasMsg & (k < 8u);
         const uint32_t sb = popq ? (1u << slot) : 0u;
         s_byte_add(r.own0, r.own1, n, 0u - sb);
         r.L &= ~sb;
-        s_byte_add(r.cnt0, r.cnt1, n, hasMsg ? 0xFFFFFFFFu : 0u);
-        r.nz &= (hasMsg && s_byte(r.cnt0, r.cnt1, n) == 0u) ? ~bit : ~0u;
+        if (CAP) s_byte_add(r.cnt0, r.cnt1, n, hasMsg ? 0xFFFFFFFFu : 0u);
+        const bool empty = CAP ? s_byte(r.cnt0, r.cnt1, n) == 0u : ((ob & ~sb) | (r.spl & bit)) == 0u;
+        r.nz &= (hasMsg & empty) ? ~bit : ~0u;
         r.msgs += hasMsg ? 1u : 0u;
         const uint32_t qn = s_qn(r.q), L = r.L;
         uint32_t adv = s_ctz((((L | (L << 8)) >> qh) & 0xFFu) | 0x100u);
         adv = adv < qn ? adv : qn;
-        r.q = (popq && k == 0u) ? ((r.q & ~0x7Fu) | ((qh + adv) & 7u) | ((qn - adv) << 3)) : r.q;
-        if (s_sq(r.q) != 0u && s_qn(r.q) < Q) ser_refill<Q>(m, r);
+        adv = (popq & (k == 0u)) ? adv : 0u;
+        r.q = (r.q & ~0x7Fu) | ((qh + adv) & 7u) | ((qn - adv) << 3);
+        if ((s_sq(r.q) != 0u) & (s_qn(r.q) < Q)) ser_refill<Q>(m, r);
     }
     ct += doIssue ? (1u << SC_IP) : 0u;
     const uint32_t op = doDump ? (uint32_t)DT_DUMP : dt_type(w);
@@ -295,21 +318,24 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
      * second; each to the tail of the receiver's inbox */
     bool ovf = false;
     auto append = [&](bool en, uint32_t d, uint32_t e) {
-        const uint32_t c = s_byte(r.cnt0, r.cnt1, d);
-        const bool over = en && (c >= cap || c >= 255u);
-        const bool ok = en && !over;
+        bool ok = en;
+        if (CAP) {
+            const uint32_t c = s_byte(r.cnt0, r.cnt1, d);
+            const bool over = en & ((c >= cap) | (c >= 255u));
+            ok = en & !over;
+            ovf = ovf | over;
+            s_byte_add(r.cnt0, r.cnt1, d, ok ? 1u : 0u);
+        }
         const uint32_t qn = s_qn(r.q);
-        const bool fast = ok && (r.q & 0xFF80u) == 0u && qn < Q;        /* no spill, a slot */
-        const uint32_t as = (s_qh(r.q) + qn) & 7u;
-        if (fast) m.st(S_Q + as, e | (d << 27));
+        const bool fast = ok & ((r.q & 0xFF80u) == 0u) & (qn < Q);     /* no spill, a slot */
+        const uint32_t as = (r.q + qn) & 7u;                           /* (qh + qn) & 7    */
+        m.st_if(fast, S_Q + as, e | (d << 27));
         const uint32_t sb = fast ? (1u << as) : 0u;
         r.L |= sb;
         s_byte_add(r.own0, r.own1, d, sb);
         r.q += fast ? (1u << 3) : 0u;
-        s_byte_add(r.cnt0, r.cnt1, d, ok ? 1u : 0u);
         r.nz |= ok ? 1u << d : 0u;
-        ovf = ovf || over;
-        if (ok && !fast) ovf = !ser_enqueue<Q>(m, r, d, e) || ovf;  /* the spill (rare)   */
+        if (ok & !fast) ovf = !ser_enqueue<Q>(m, r, d, e) || ovf;  /* the spill (rare)   */
     };
     {
         uint32_t dm = o.o0 >> 24;

@@ -31,6 +31,7 @@ struct HostCol {
     uint32_t *spill;                     /* [S_SPILL] */
     uint32_t ld(uint32_t w) const { return p[w]; }
     void st(uint32_t w, uint32_t v) const { p[w] = v; }
+    void st_if(bool en, uint32_t w, uint32_t v) const { if (en) p[w] = v; }
     uint32_t ld8(uint32_t w, uint32_t b) const { return reinterpret_cast<const uint8_t *>(&p[w])[b]; }
     void st8(uint32_t w, uint32_t b, uint32_t v) const { reinterpret_cast<uint8_t *>(&p[w])[b] = (uint8_t)v; }
     uint32_t ld16(uint32_t w, uint32_t h) const { return reinterpret_cast<const uint16_t *>(&p[w])[h]; }
@@ -92,7 +93,8 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         uint32_t v;
         bool sp = false;
         do {
-            v = dsms::ser_step<NP, Q>(m, r, T, fetch, on_dump, lim, cap);
+            v = cap < 256u ? dsms::ser_step<NP, Q, true>(m, r, T, fetch, on_dump, lim, cap)
+                           : dsms::ser_step<NP, Q, false>(m, r, T, fetch, on_dump, lim, cap);
             sp = sp || dsms::s_sq(r.q) != 0u;
         } while (v == dsms::SR_RUN);
         spilled += sp;

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # tools/build_base.sh [rev] -- build libdsm.so of git revision `rev` (default HEAD) into
-# abtmp/libdsm_base.so, for an A/B against the working tree with tools/ab_lib.sh
+# ab/libdsm_${NAME:-base}.so, for an A/B against the working tree with tools/ab_lib.sh
 set -e
 REV=${1:-HEAD}
 T=$(mktemp -d)
@@ -9,7 +9,7 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$T/include"
 $H -c "$T/hp-assignment-2_amd/csrc/dsm_engine.hip" -o "$T/e.o" 2>/dev/null
 $H -c "$T/hp-assignment-2_amd/csrc/dsm_text.hip" -o "$T/t.o" 2>/dev/null
 gcc -O2 -fPIC -std=gnu11 -I"$T/include" -c "$T/hp-assignment-2_amd/csrc/dsm_host.c" -o "$T/h.o"
-mkdir -p abtmp
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$T/e.o" "$T/t.o" "$T/h.o" -o abtmp/libdsm_base.so
+mkdir -p ab
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$T/e.o" "$T/t.o" "$T/h.o" -o ab/libdsm_${NAME:-base}.so
 rm -rf "$T"
-echo "abtmp/libdsm_base.so <- $REV"
+echo "ab/libdsm_${NAME:-base}.so <- $REV"
