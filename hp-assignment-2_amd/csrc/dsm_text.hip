@@ -269,10 +269,8 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
                                                       uint32_t *counts, int32_t *status) {
     constexpr uint32_t K = BPL / 16, WIN = 64 * BPL;
     __shared__ __attribute__((aligned(16))) uint8_t s_txt[PW][WIN + PHALO + 16];
-    __shared__ uint16_t s_list[PW][WIN];                /* chunk offsets of the window */
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint8_t *const st = s_txt[wv];
-    uint16_t *const sl = s_list[wv];
     for (uint64_t f = (uint64_t)blockIdx.x * PW + wv; f < n_files; f += (uint64_t)gridDim.x * PW) {
         const uint64_t b0 = off[f], b1 = off[f + 1];
         uint16_t *const out = traces + f * stride;
@@ -333,7 +331,8 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
             const uint32_t r = ~nl & fm;
             const uint32_t t1 = r & (r >> 1), t2 = t1 & (t1 >> 2), t4 = t2 & (t2 >> 4), t8 = t4 & (t4 >> 8);
             const bool run19 = BPL > DP_CHUNK && (t8 & (t1 >> 16) & (r >> 18)) != 0u;
-            if ((lo == 0 && din + (fnl < BPL - 1u ? fnl : BPL - 1u) >= DP_CHUNK) || run19) {   /* long line */
+            /* (lanes past the file's end have no bytes: fm == 0 keeps them out) */
+            if (fm != 0u && ((lo == 0 && din + (fnl < BPL - 1u ? fnl : BPL - 1u) >= DP_CHUNK) || run19)) {   /* long line */
                 uint32_t d = din % DP_CHUNK;
                 cs = 0;
                 for (uint32_t j = 0; j < BPL; ++j) {
@@ -342,22 +341,21 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
                     d = ((nl >> j) & 1u) ? 0u : (d == DP_CHUNK - 1 ? 0u : d + in);
                 }
             }
-            /* (5) compact the chunk starts of the window (window order = instruction order) */
+            /* (5) instruction indices: a wave prefix sum of the chunk starts per lane (window
+             * order = instruction order) */
             const uint32_t nc = __builtin_popcount(cs);
             const uint32_t isum = wave_incl_sum(nc);
             const uint32_t T = __builtin_amdgcn_readlane(isum, 63);
-            {
-                uint32_t k = isum - nc;
-                for (uint32_t m = cs; m; m &= m - 1u) sl[k++] = (uint16_t)(BPL * lane + __builtin_ctz(m));
-            }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            /* (6) one chunk per lane per round: parse from LDS, coalesced 2-byte stores */
+            /* (6) each lane parses the chunks that start in its bytes, one per round, from
+             * LDS (no compaction pass: about as many rounds, ~3 of the ~4 lines per lane),
+             * 2-byte stores at their instruction index */
             const uint32_t tmax = cap - idx0 < T ? cap - idx0 : T;
             const uint32_t rem = e0 - wr0;                       /* file bytes from wa on */
-            for (uint32_t t0 = 0; t0 < tmax; t0 += 64) {
-                const uint32_t t = t0 + lane;
-                if (t < tmax) {
-                    const uint32_t o = sl[t];
+            uint32_t mcs = cs, t = isum - nc;
+            while (__ballot((mcs != 0u) & (t < tmax))) {
+                if ((mcs != 0u) & (t < tmax)) {
+                    const uint32_t o = BPL * lane + (uint32_t)__builtin_ctz(mcs);
                     const uint32_t lim = rem - o < DP_CHUNK ? rem - o : DP_CHUNK;
                     const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
                     const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
@@ -378,6 +376,8 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
                         err = e < err ? e : err;
                     }
                 }
+                mcs &= mcs - 1u;
+                ++t;
             }
             if (__ballot(err != 0xFFFFFFFFu)) err = wave_min(err);
             idx0 += T;

@@ -12,6 +12,9 @@
 #   abl:DIST:N:LIB,LIB          tools/ab_libs.sh (variant builds, "default" = the tree's)
 #   util:LIB:DIST               tools/lane_util.py on an instrumented build
 #   parse                       GPU text tests, tools/ab_parse.py, tools/prof_parse.sh
+#   parsel:LIB,LIB              tools/ab_parse.py per build ("default" = the tree's), twice
+#   pipe:N:DIST:PARTS           tools/ab_pipe.py: one engine vs the ensemble in PARTS streams
+#   calib                       FETCH_SIZE of a known per-lane 16-B chunk read (ab/calib_fetch)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() {   # step <log name> <seconds> <command...>
@@ -40,6 +43,17 @@ for s in "$@"; do
     parse)   step text_tests 600 python -u -m pytest tests/test_gpu_text.py -x -q --timeout 240 --timeout-method thread
              step ab_parse 300 python -u tools/ab_parse.py 65536 5
              bash tools/prof_parse.sh new || exit $? ;;
+    parsel)  for r in 1 2; do for L in ${a//,/ }; do
+                 if [ "$L" = default ]; then L=""; fi
+                 step "parse_${r}_$(basename "${L:-default}" .so)" 300 env DSM_LIB="$L" python -u tools/ab_parse.py 65536 5
+             done; done ;;
+    pipe)    step "pipe_${b}_$c" 600 python -u tools/ab_pipe.py "$a" 3 "$b" "$c" ;;
+    calib)   for cfg in "1048576 64 0" "1048576 64 256" "1048576 8 256" "262144 256 64"; do
+                 set -- $cfg
+                 d=gpurun_out/calib/l$1_c$2_a$3
+                 step "calib_l$1_c$2_a$3" 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$d" \
+                     -o calib -- ab/calib_fetch "$1" "$2" "$3"
+             done ;;
     *)       echo "tools/gpu.sh: unknown step $s"; exit 2 ;;
     esac
 done
