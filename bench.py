@@ -405,12 +405,11 @@ def main():
         # the packed path runs the transition kernel as two launches per step (budget pass +
         # resume pass, run_engine's two-pass schedule): bytes and time are per step, i.e. the
         # sum over both launches (rocprof lists 2 sim_kernel dispatches per step)
-        launches = 2 if li.get("resume_blocks") else 1
-        # which kernel of the fast-forward / plain pair ran (dsm_set_fast_forward AUTO); with
-        # the plain one the resume pass runs in serial form (ser_kernel, one lane per system)
-        ff_picked = (local_c["ff_sample_runs"] > 0 and
-                     16 * local_c["ff_sample_runs"] >= local_c["ff_sample_instrs"]) or args.fused
-        serial = launches == 2 and not ff_picked and os.environ.get("DSM_SERIAL", "1") != "0"
+        launches = 2 if li.get("resume_form") else 1
+        # which kernel of the fast-forward / plain pair ran (the trace scan's verdict, read
+        # back by dsm_launch_info_get) and which resume pass followed the budget pass
+        ff_picked = li.get("ff_picked") == 1 or args.fused
+        serial = li.get("resume_form") == 2
         roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
                     kernel=(("sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain) budget pass "
@@ -421,7 +420,8 @@ def main():
                             ("sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel with the hit-run fast-forward"
                              if ff_picked else "sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain")
                             + "; 4-wave groups, ring 12, packed traces; picked per run by ffscan_kernel's trace sample)"
-                            + (f"; budget pass (2^{li['budget_log2']} rounds) + resume pass" if launches == 2 else "")
+                            + (f"; budget pass ({li['budget_rounds']} rounds) + resume pass ({pydsm.RESUME_FORMS[li['resume_form']]})"
+                               if launches == 2 else "")
                             + (" in serial form (ser_kernel<8>: one lane per suspended system)" if serial else "")),
                     launches_per_step=launches,
                     algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),

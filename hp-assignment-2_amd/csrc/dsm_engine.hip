@@ -1595,6 +1595,21 @@ extern "C" void dsm_close(dsm_ctx *c) {
 
 extern "C" int dsm_launch_info_get(dsm_ctx *c, dsm_launch_info *info) {
     if (!c || !info) return DSM_E_INVAL;
+    if (c->last_pair && c->last_blog) {
+        /* the trace scan chose the pair's kernel on the device: wait for the run, read the
+         * verdict (ff_verdict) and report the passes that actually ran */
+        uint32_t scan[2] = {0, 0};
+        HIPCK(hipSetDevice(c->device));
+        HIPCK(hipStreamSynchronize(c->last_st));
+        HIPCK(hipMemcpy(scan, c->d_ctrl + CTRL_SCAN, sizeof scan, hipMemcpyDeviceToHost));
+        const bool ff = scan[1] != 0u && (uint64_t)scan[1] * 16u >= scan[0];
+        c->info.ff_picked = ff ? 1 : 0;
+        c->info.resume_form = ff ? DSM_RESUME_FASTFORWARD
+                                 : (c->last_use_ser ? DSM_RESUME_SERIAL : DSM_RESUME_LOCKSTEP);
+        c->info.resume_blocks = (ff || !c->last_use_ser) ? c->last_grid_fast : c->cus;
+        c->info.budget_rounds = (int)((ff && c->last_thr_ff) ? c->last_thr_ff : 1u << c->last_blog);
+        c->last_pair = 0;
+    }
     *info = c->info;
     return DSM_OK;
 }
@@ -1815,6 +1830,20 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     c->info.ring_cap = ring_eff;
     c->info.resume_blocks = blog ? (use_ser ? c->cus : grid_fast) : 0;
     c->info.budget_log2 = (int)blog;
+    /* without the pair the host knows the passes; with it, dsm_launch_info_get reads the
+     * device's verdict */
+    const bool ff_kernel = !plain_only && (mode & (M_TR | M_SX)) == 0;   /* step (0) compiled in */
+    c->info.ff_picked = ff_kernel ? 1 : 0;
+    c->info.resume_form = !blog ? DSM_RESUME_NONE
+                        : use_ser ? DSM_RESUME_SERIAL
+                        : (ff_kernel ? DSM_RESUME_FASTFORWARD : DSM_RESUME_LOCKSTEP);
+    c->info.budget_rounds = blog ? (int)((ff_kernel && A.thr_ff) ? A.thr_ff : 1u << blog) : 0;
+    c->last_st = st;
+    c->last_pair = pair ? 1 : 0;
+    c->last_use_ser = use_ser ? 1 : 0;
+    c->last_grid_fast = grid_fast;
+    c->last_blog = blog;
+    c->last_thr_ff = A.thr_ff;
     c->info.lds_bytes_per_block = lds_bytes(ring_eff, FW);
     c->info.late_log2 = (int)A.late_rsh;
     c->info.round_limit_log2 = (int)c->round_limit_log2;

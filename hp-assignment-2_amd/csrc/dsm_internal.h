@@ -46,6 +46,11 @@ struct dsm_ctx {
     hipEvent_t tev0[DSM_TIMING_RING], tev1[DSM_TIMING_RING];
     uint64_t runs_timed;
     dsm_launch_info info;
+    /* the last run's pass choice when the device picks it (DSM_FF_AUTO): dsm_launch_info_get
+     * reads the trace scan's verdict after waiting for last_st */
+    hipStream_t last_st;
+    int last_pair, last_use_ser, last_grid_fast;
+    uint32_t last_blog, last_thr_ff;
     /* two-pass schedule and round limit (dsm_set_budget / dsm_set_round_limit; defaults from
      * DSM_BUDGET_LOG2 / DSM_LATE_LOG2, read once at dsm_open) */
     uint32_t budget_log2, late_log2, round_limit_log2, inbox_limit;

@@ -276,7 +276,7 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
         adv = adv < qn ? adv : qn;
         adv = (popq & (k == 0u)) ? adv : 0u;
         r.q = (r.q & ~0x7Fu) | ((qh + adv) & 7u) | ((qn - adv) << 3);
-        if ((s_sq(r.q) != 0u) & (s_qn(r.q) < Q)) ser_refill<Q>(m, r);
+        if ((uint32_t)(s_sq(r.q) != 0u) & (uint32_t)(s_qn(r.q) < Q)) ser_refill<Q>(m, r);
     }
     ct += doIssue ? (1u << SC_IP) : 0u;
     const uint32_t op = doDump ? (uint32_t)DT_DUMP : dt_type(w);

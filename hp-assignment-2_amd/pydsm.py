@@ -62,7 +62,12 @@ class LaunchInfo(ctypes.Structure):
                 ("ring_cap", ctypes.c_int), ("lds_bytes_per_block", ctypes.c_int),
                 ("resume_blocks", ctypes.c_int), ("budget_log2", ctypes.c_int),
                 ("late_log2", ctypes.c_int), ("round_limit_log2", ctypes.c_int),
-                ("fmt_tile", ctypes.c_int), ("parse_bpl", ctypes.c_int)]
+                ("fmt_tile", ctypes.c_int), ("parse_bpl", ctypes.c_int),
+                ("resume_form", ctypes.c_int), ("budget_rounds", ctypes.c_int),
+                ("ff_picked", ctypes.c_int)]
+
+
+RESUME_FORMS = {0: "none", 1: "lock-step", 2: "serial", 3: "fast-forward lock-step"}
 
 
 _lib = None

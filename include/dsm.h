@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DSM_ABI_VERSION 2
+#define DSM_ABI_VERSION 3   /* 3: dsm_launch_info grew resume_form / budget_rounds / ff_picked */
 
 #define DSM_MAX_NP 8             /* bitVector is one byte (README.md:51)                  */
 #define DSM_CACHE_SIZE 4         /* CACHE_SIZE      assignment.c:10                        */
@@ -164,13 +164,24 @@ typedef struct dsm_launch_info {
     int cus;
     int ring_cap;
     int lds_bytes_per_block;
-    int resume_blocks;     /* two-pass schedule: workgroups of the resume pass (0: none)   */
-    int budget_log2;       /* its budget pass's round budget, log2 (0: one pass)          */
+    int resume_blocks;     /* two-pass schedule: workgroups of the resume pass that ran
+                            * (0: none; the serial form runs one per CU)                    */
+    int budget_log2;       /* the plain budget pass's round budget, log2 (0: one pass)     */
     int late_log2;         /* the budget once a wave finds no new system, log2 (0: none)   */
     int round_limit_log2;  /* ROUND_LIMIT after 1 << this many active rounds               */
     int fmt_tile;          /* dump formatter tile (DSM_FMT at dsm_open)                   */
     int parse_bpl;         /* trace parser bytes per lane per window (DSM_PARSE_BPL)       */
+    /* ABI 3: which passes ran.  With DSM_FF_AUTO the trace scan decides on the device, so
+     * dsm_launch_info_get waits for the last run's stream to read its verdict. */
+    int resume_form;       /* DSM_RESUME_*: the resume pass that ran                        */
+    int budget_rounds;     /* the budget pass's effective budget in rounds (0: one pass):
+                            * 1 << budget_log2, or the fast-forward budget (384) when the
+                            * scan picked the hit-run fast-forward                           */
+    int ff_picked;         /* 1 when the hit-run fast-forward kernel carried the run        */
 } dsm_launch_info;
+
+enum { DSM_RESUME_NONE = 0, DSM_RESUME_LOCKSTEP = 1, DSM_RESUME_SERIAL = 2,
+       DSM_RESUME_FASTFORWARD = 3 };
 
 /* ---- library ---------------------------------------------------------------------- */
 int dsm_abi_version(void);
@@ -237,8 +248,10 @@ int dsm_get_issue_trace(dsm_ctx *ctx, uint64_t sys, uint32_t *events, uint32_t c
 int dsm_format_issue_trace(const uint32_t *events, uint32_t n, char *buf, size_t cap);
 
 /* Device time of the transition kernel of the last run (needs DSM_F_TIMING): HIP events
- * recorded on the run's own stream right before and after its launches (budget + resume
- * pass).  Waits for the stop event. */
+ * recorded on the run's own stream right before and after its launches.  The window holds
+ * every launch of the budget and resume passes: with DSM_FF_AUTO on the packed path that is
+ * the trace scan (ffscan_kernel, ~0.02 ms) and both kernels of each fast-forward / plain pair,
+ * one of which exits at once (a few microseconds).  Waits for the stop event. */
 int dsm_last_kernel_ms(dsm_ctx *ctx, float *ms);
 /* The same for the last min(cap, runs, 64) runs, oldest first; *n = how many. */
 int dsm_kernel_ms_history(dsm_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);

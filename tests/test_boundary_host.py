@@ -42,7 +42,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_errors():
     L = pydsm.lib()
-    assert L.dsm_abi_version() == 2
+    assert L.dsm_abi_version() == 3
     assert pydsm.strerror(0) == "ok"
     for code in range(-7, 0):
         assert pydsm.strerror(code) != "unknown error"

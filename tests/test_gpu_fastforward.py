@@ -45,6 +45,7 @@ def test_packed_fast_forward_vs_oracle(dsm, orc, np_, dist, ring):
     tr, cn = orc.generate(np_, dist, 17, 4096, 123, n)
     with dsm.Engine(np_, 4096, ring_cap=ring, snapshots=True) as eng:
         res, cnt = eng.run_packed(tr, cn)
+        info = eng.launch_info()
         ores, _, odump, ofin = orc.run_packed(np_, tr, cn, records=True, nthreads=16)
         for s in range(0, n, 61):
             mask = int(ores[s]["status"]) >> 8
@@ -57,6 +58,11 @@ def test_packed_fast_forward_vs_oracle(dsm, orc, np_, dist, ring):
     assert cnt["msgs"] == int(ores["msgs"].sum()) and cnt["instrs"] == int(ores["instrs"].sum())
     if dist == "hot":
         assert cnt["ff_passes"] > 0 and cnt["ff_steps"] > 0
+        # the trace scan picked the fast-forward pair: its kernel ran both passes' resume
+        assert info["ff_picked"] == 1 and info["resume_form"] == 3, info
+        assert info["resume_blocks"] == info["grid_blocks"] and info["budget_rounds"] == 384, info
+    else:
+        assert info["ff_picked"] == 0 and info["resume_form"] == 2, info
 
 
 def test_fast_forward_equals_round_by_round(dsm, orc):
