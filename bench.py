@@ -58,7 +58,7 @@ def shard(rank, n_per_rank):
 def reduce_counters(vec, dist_mod=None):
     """All-reduce a 32-entry uint64 counter vector across ranks: sums (mod 2^64) for every
     slot except max_rounds (slot 24), which is a max.  `vec` is a torch int64 tensor."""
-    if dist_mod is None or not dist_mod.is_initialized() or dist_mod.get_world_size() == 1:
+    if dist_mod is None or not dist_mod.is_initialized():
         return vec
     mx = vec[24:25].clone()
     dist_mod.all_reduce(vec, op=dist_mod.ReduceOp.SUM)
@@ -253,7 +253,10 @@ def main():
     if os.environ.get("DSM_BENCH_DEVICE"):
         local = int(os.environ["DSM_BENCH_DEVICE"])
     backend = os.environ.get("DSM_BENCH_BACKEND", "nccl")     # nccl = RCCL over xGMI
-    if world > 1:
+    # DSM_BENCH_DIST=1: the process group and its collectives even at one rank -- on a
+    # one-GPU box that runs the RCCL init / barrier / all-reduce path end to end
+    use_dist = world > 1 or os.environ.get("DSM_BENCH_DIST") == "1"
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -307,14 +310,14 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()          # asynchronous: the steps queue back to back on the stream
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     # the transition kernel's device time per step (HIP events around its launches, on the
@@ -386,11 +389,11 @@ def main():
 
     cdev = dev if backend == "nccl" else torch.device("cpu")    # gloo: host tensors
     el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-    if world > 1:
+    if use_dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed_max = float(el.item())
     local_c = pydsm.counters_to_dict(cnt.cpu().numpy().view(np.uint64))
-    tot = reduce_counters(cnt.clone().to(cdev), dist if world > 1 else None)
+    tot = reduce_counters(cnt.clone().to(cdev), dist if use_dist else None)
     c = pydsm.counters_to_dict(tot.cpu().numpy().view(np.uint64))
 
     if rank == 0:
@@ -523,11 +526,13 @@ def main():
             "kernel_ms": [round(x, 3) for x in kms],
             "sum_final_hash": hex(c["sum_final_hash"]),
             "parity": parity,
+            "collective": (("rccl" if backend == "nccl" else backend) + f" all_reduce of 32 counters over {world} rank(s)")
+                          if use_dist else None,
             "launch": eng.launch_info(),
         }
         print(json.dumps(rec), flush=True)
     eng.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -1,6 +1,7 @@
-"""GPU: bench.py end to end on the one GPU of the box -- the 1-rank line, and `--gpus 2`
-through its own launcher (both ranks on device 0, counters over gloo: RCCL needs a GPU per
-rank), whose whole-job counters must equal one rank simulating both shards."""
+"""GPU: bench.py end to end on the one GPU of the box -- the 1-rank line, `--gpus 2` through
+its own launcher (both ranks on device 0, counters over gloo: RCCL needs a GPU per rank), whose
+whole-job counters must equal one rank simulating both shards, and the RCCL path (process
+group, barriers, all-reduce of the counters and of the elapsed time) at one rank."""
 import json
 import os
 import subprocess
@@ -36,3 +37,22 @@ def test_two_rank_launch_equals_one_rank_over_both_shards():
         assert two["counters"][k] == one["counters"][k], k
     assert two["sum_final_hash"] == one["sum_final_hash"]
     assert two["value"] > 0 and two["roofline"]["achieved"] > 0
+
+
+def test_rccl_collective_path_one_rank():
+    """bench.py's torch.distributed path on the nccl backend (RCCL), forced at world size 1:
+    init with device_id, the barriers around the timed region, the MAX all-reduce of the
+    elapsed time and the SUM / MAX all-reduce of the counters -- the same results as the plain
+    run."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "LOCAL_WORLD_SIZE": "1",
+           "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "DSM_BENCH_DIST": "1"}
+    rccl = _bench(["--gpus", "1"] + SMALL, env=env)
+    plain = _bench(["--gpus", "1"] + SMALL)
+    assert rccl["collective"].startswith("rccl all_reduce") and plain["collective"] is None
+    for k in ("msgs", "instrs", "rounds", "systems", "max_rounds", "status_DEADLOCKED"):
+        assert rccl["counters"][k] == plain["counters"][k], k
+    assert rccl["sum_final_hash"] == plain["sum_final_hash"]
