@@ -1606,7 +1606,7 @@ extern "C" int dsm_launch_info_get(dsm_ctx *c, dsm_launch_info *info) {
         c->info.ff_picked = ff ? 1 : 0;
         c->info.resume_form = ff ? DSM_RESUME_FASTFORWARD
                                  : (c->last_use_ser ? DSM_RESUME_SERIAL : DSM_RESUME_LOCKSTEP);
-        c->info.resume_blocks = (ff || !c->last_use_ser) ? c->last_grid_fast : c->cus;
+        c->info.resume_blocks = (ff || !c->last_use_ser) ? c->last_grid_fast : c->last_ser_blocks;
         c->info.budget_rounds = (int)((ff && c->last_thr_ff) ? c->last_thr_ff : 1u << c->last_blog);
         c->last_pair = 0;
     }
@@ -1686,7 +1686,12 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     }
     if ((rc = ensure(&c->d_recs, &c->recs_cap, (size_t)n_sys * np * 8))) return rc;
     /* the serial pass's spill FIFOs: S_SPILL words per lane (96 MiB on 256 CUs) */
-    if (use_ser && (rc = ensure(&c->d_spill, &c->spill_cap, (size_t)c->cus * 64 * SER_WAVES * dsms::S_SPILL))) return rc;
+    /* the serial pass's grid: one workgroup per CU, fewer when the ensemble cannot fill
+     * them (at most n_sys systems are suspended); its spill FIFOs: S_SPILL words per lane
+     * (96 MiB on 256 CUs, 384 KiB per workgroup) */
+    const int ser_blocks = (int)((uint64_t)c->cus < (n_sys + 64 * SER_WAVES - 1) / (64 * SER_WAVES)
+                                     ? (uint64_t)c->cus : (n_sys + 64 * SER_WAVES - 1) / (64 * SER_WAVES));
+    if (use_ser && (rc = ensure(&c->d_spill, &c->spill_cap, (size_t)ser_blocks * 64 * SER_WAVES * dsms::S_SPILL))) return rc;
     if (!d_results) {   /* the engine needs the per-system header even if the caller does not */
         if ((rc = ensure(&c->d_res, &c->res_cap, (size_t)n_sys + 1))) return rc;
         d_results = c->d_res;
@@ -1799,7 +1804,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
             const bool capb = c->inbox_limit < (uint32_t)FB_RING;
             hipLaunchKernelGGL(np == 4 ? (capb ? ser_kernel<4, true> : ser_kernel<4, false>)
                                        : (capb ? ser_kernel<8, true> : ser_kernel<8, false>),
-                               dim3(c->cus), dim3(64 * SER_WAVES), 0, st, a);
+                               dim3(ser_blocks), dim3(64 * SER_WAVES), 0, st, a);
             HIPCK(hipGetLastError());
         } else if (pair) {
             hipLaunchKernelGGL(fast_nf, dim3(grid_fast), dim3(64 * FW), 0, st, a);
@@ -1828,7 +1833,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     c->info.waves_per_cu = nb_fast * FW;
     c->info.cus = c->cus;
     c->info.ring_cap = ring_eff;
-    c->info.resume_blocks = blog ? (use_ser ? c->cus : grid_fast) : 0;
+    c->info.resume_blocks = blog ? (use_ser ? ser_blocks : grid_fast) : 0;
     c->info.budget_log2 = (int)blog;
     /* without the pair the host knows the passes; with it, dsm_launch_info_get reads the
      * device's verdict */
@@ -1842,6 +1847,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     c->last_pair = pair ? 1 : 0;
     c->last_use_ser = use_ser ? 1 : 0;
     c->last_grid_fast = grid_fast;
+    c->last_ser_blocks = ser_blocks;
     c->last_blog = blog;
     c->last_thr_ff = A.thr_ff;
     c->info.lds_bytes_per_block = lds_bytes(ring_eff, FW);

@@ -49,7 +49,7 @@ struct dsm_ctx {
     /* the last run's pass choice when the device picks it (DSM_FF_AUTO): dsm_launch_info_get
      * reads the trace scan's verdict after waiting for last_st */
     hipStream_t last_st;
-    int last_pair, last_use_ser, last_grid_fast;
+    int last_pair, last_use_ser, last_grid_fast, last_ser_blocks;
     uint32_t last_blog, last_thr_ff;
     /* two-pass schedule and round limit (dsm_set_budget / dsm_set_round_limit; defaults from
      * DSM_BUDGET_LOG2 / DSM_LATE_LOG2, read once at dsm_open) */

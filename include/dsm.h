@@ -165,7 +165,8 @@ typedef struct dsm_launch_info {
     int ring_cap;
     int lds_bytes_per_block;
     int resume_blocks;     /* two-pass schedule: workgroups of the resume pass that ran
-                            * (0: none; the serial form runs one per CU)                    */
+                            * (0: none; the serial form runs one per CU, fewer when
+                            * n_sys < 384 per CU, with a 384-KiB inbox spill area each)     */
     int budget_log2;       /* the plain budget pass's round budget, log2 (0: one pass)     */
     int late_log2;         /* the budget once a wave finds no new system, log2 (0: none)   */
     int round_limit_log2;  /* ROUND_LIMIT after 1 << this many active rounds               */
