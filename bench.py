@@ -423,8 +423,7 @@ def main():
                             ("sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel with the hit-run fast-forward"
                              if ff_picked else "sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain")
                             + "; 4-wave groups, ring 12, packed traces; picked per run by ffscan_kernel's trace sample)"
-                            + (f"; budget pass ({li['budget_rounds']} rounds) + resume pass ({pydsm.RESUME_FORMS[li['resume_form']]})"
-                               if launches == 2 else "")
+                            + (f"; budget pass ({li['budget_rounds']} rounds) + resume pass" if launches == 2 else "")
                             + (" in serial form (ser_kernel<8>: one lane per suspended system)" if serial else "")),
                     launches_per_step=launches,
                     algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),

@@ -40,6 +40,21 @@ def test_library_exports_every_header_symbol():
     assert set(header_functions()) <= exported
 
 
+def _struct_fields(name):
+    txt = open(os.path.join(REPO, "include", "dsm.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), txt, flags=re.S).group(1)
+    return re.findall(r"\b(\w+)\s*;", body)
+
+
+def test_launch_info_binding_matches_header():
+    """pydsm's ctypes mirror of dsm_launch_info (ABI 3) has the header's fields in order,
+    all of them int, so the library never writes past the caller's struct."""
+    assert [f for f, _ in pydsm.LaunchInfo._fields_] == _struct_fields("dsm_launch_info")
+    assert ctypes.sizeof(pydsm.LaunchInfo) == 4 * len(_struct_fields("dsm_launch_info"))
+    assert set(pydsm.RESUME_FORMS) == {0, 1, 2, 3}
+
+
 def test_abi_version_and_errors():
     L = pydsm.lib()
     assert L.dsm_abi_version() == 3
