@@ -12,12 +12,14 @@
  *                synthetic core files in the shipped tests' text format, from the
  *                counter-based generator (bench and test inputs for parse_kernel).
  *
- * parse_kernel: one wave per file, 1 KB windows (16 B per lane, aligned loads, staged in
- * LDS with a 32-byte halo).  A chunk starts at each line start and every 19 bytes into a
- * longer line; every lane finds the chunk starts among its 16 bytes (distance to the line
- * start mod 19, the line start carried across lanes by a wave max-scan), a wave prefix sum
- * gives each chunk its instruction index, and each lane parses its chunks from LDS.  The first
- * failing chunk (by index) ends the file, as the reference's loop would have misbehaved there.
+ * parse_kernel: one wave per file (one-wave workgroups), 2 KB windows (32 B per lane, aligned
+ * loads, staged in LDS with a 32-byte halo).  A chunk starts at each line start and every 19
+ * bytes into a longer line; every lane finds the chunk starts among its 32 bytes (distance
+ * to the line start mod 19, the line start carried across lanes by a wave max-scan), a wave
+ * prefix sum gives each chunk its instruction index, and each lane decodes the chunks that
+ * start in its bytes from LDS with the canonical-line fast path; chunks it declines are
+ * scanned exactly (dsm_parse.h) after that loop.  The first failing chunk (by index) ends the
+ * file, as the reference's loop would have misbehaved there.
  *
  * Layout of one dump (Appendix C of SURVEY.md): the memory and directory sections are fixed
  * width (%3d / %02X / %5d / %2s / %08X of byte-sized fields), so only the cache section moves:
@@ -181,7 +183,11 @@ __global__ void __launch_bounds__(NT) fmt_kernel(const uint8_t *recs, uint64_t r
 
 
 /* ---- trace parser ------------------------------------------------------------------- */
-constexpr uint32_t PHALO = 32, PW = 4;   /* halo bytes (a chunk is <= 19), waves/group */
+constexpr uint32_t PHALO = 32;      /* halo bytes (a chunk is <= 19) */
+#ifndef PARSE_PW
+#define PARSE_PW 1          /* one-wave workgroups: 1 / 2 / 4 / 8 measured 9.43 / 9.70 / 9.68 / 9.70 ms */
+#endif
+constexpr uint32_t PW = PARSE_PW;   /* waves per workgroup */
 
 /* aligned 16-byte load through the global address space (in-order vmcnt, not flat) */
 DEVI uint4 ldg16(const uint8_t *p) {
@@ -352,10 +358,13 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
              * 2-byte stores at their instruction index */
             const uint32_t tmax = cap - idx0 < T ? cap - idx0 : T;
             const uint32_t rem = e0 - wr0;                       /* file bytes from wa on */
-            uint32_t mcs = cs, t = isum - nc;
+            /* the fast path only, in a tight loop; the chunks it declines (any other shape,
+             * an address whose home is >= np) are marked in `slow` and scanned exactly after
+             * the loop -- inside it, the rare branch's code and registers slowed every round */
+            uint32_t mcs = cs, t = isum - nc, slow = 0;
             while (__ballot((mcs != 0u) & (t < tmax))) {
                 if ((mcs != 0u) & (t < tmax)) {
-                    const uint32_t o = BPL * lane + (uint32_t)__builtin_ctz(mcs);
+                    const uint32_t b = (uint32_t)__builtin_ctz(mcs), o = BPL * lane + b;
                     const uint32_t lim = rem - o < DP_CHUNK ? rem - o : DP_CHUNK;
                     const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
                     const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
@@ -363,21 +372,28 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
                     const uint32_t c1 = __builtin_amdgcn_alignbyte(d2, d1, o & 3u);
                     const uint32_t c2 = __builtin_amdgcn_alignbyte(d3, d2, o & 3u);
                     uint32_t pk = 0;
-                    int rc = 0;
-                    if (!parse_fast(c0, c1, c2, lim, &pk)) {
-                        uint32_t len = 0;
-                        while (len < lim) { if (st[o + len++] == '\n') break; }
-                        rc = dp_parse_chunk_at([&](uint32_t i) -> uint32_t { return i < len ? (uint32_t)st[o + i] : 0u; }, &pk);
-                    }
-                    if (rc == 0 && ((pk >> 12) & 7u) >= (uint32_t)np) rc = DSM_E_RANGE;   /* home < np */
-                    if (rc == 0) out[idx0 + t] = (uint16_t)pk;
-                    else {
-                        const uint32_t e = (idx0 + t) * 8u + (rc == DSM_E_FORMAT ? 1u : 2u);
-                        err = e < err ? e : err;
-                    }
+                    const bool ok = parse_fast(c0, c1, c2, lim, &pk) & (((pk >> 12) & 7u) < (uint32_t)np);
+                    if (ok) out[idx0 + t] = (uint16_t)pk;
+                    slow |= ok ? 0u : 1u << b;
                 }
                 mcs &= mcs - 1u;
                 ++t;
+            }
+            if (__ballot(slow != 0u)) {
+                for (uint32_t m = slow; m; m &= m - 1u) {
+                    const uint32_t b = (uint32_t)__builtin_ctz(m), o = BPL * lane + b;
+                    const uint32_t ti = isum - nc + (uint32_t)__builtin_popcount(cs & lowmask(b));
+                    const uint32_t lim = rem - o < DP_CHUNK ? rem - o : DP_CHUNK;
+                    uint32_t pk = 0, len = 0;
+                    while (len < lim) { if (st[o + len++] == '\n') break; }
+                    int rc = dp_parse_chunk_at([&](uint32_t i) -> uint32_t { return i < len ? (uint32_t)st[o + i] : 0u; }, &pk);
+                    if (rc == 0 && ((pk >> 12) & 7u) >= (uint32_t)np) rc = DSM_E_RANGE;   /* home < np */
+                    if (rc == 0) out[idx0 + ti] = (uint16_t)pk;
+                    else {
+                        const uint32_t e = (idx0 + ti) * 8u + (rc == DSM_E_FORMAT ? 1u : 2u);
+                        err = e < err ? e : err;
+                    }
+                }
             }
             if (__ballot(err != 0xFFFFFFFFu)) err = wave_min(err);
             idx0 += T;
