@@ -158,3 +158,16 @@ def test_serial_assert_home_beyond_np(dsm, orc, monkeypatch):
                 assert np.array_equal(eng.node_state(s, nd)[1], ofin[s, nd]), (s, nd)
     _cmp(res, ores)
     assert cnt["status_ASSERT_FAILED"] == nasr and cnt["resumed"] > 0
+
+
+@pytest.mark.parametrize("n", [1, 7, 385, 1537])
+def test_serial_small_ensembles(dsm, orc, monkeypatch, n):
+    """Ensembles that fill less than a CU's serial workgroup (384 lanes) or spill into a few:
+    the serial grid and its inbox spill area are sized by ceil(n / 384) workgroups, and every
+    system still reaches the oracle's result (budget 2^4: almost all of them resumed)."""
+    tr, cn = orc.generate(8, "uniform", 23, 4096, 500, n)
+    ores, _ = orc.run_packed(8, tr, cn, nthreads=8)[:2]
+    res, cnt, info, _ = _run(dsm, monkeypatch, 8, tr, cn, True, 4)
+    _cmp(res, ores)
+    assert info["resume_form"] == 2 and info["resume_blocks"] == min(info["cus"], -(-n // 384)), info
+    assert cnt["systems"] == n and cnt["resumed"] > 0
