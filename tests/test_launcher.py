@@ -49,3 +49,19 @@ def test_host_cpu_description():
     hc = bench.host_cpu()
     assert hc["threads"] >= 1 and hc["nproc"] >= hc["affinity"] >= 1
     assert isinstance(hc["model"], str)
+
+
+def test_host_cpu_respects_the_job_share(monkeypatch):
+    """The CPU baselines run on the job's CPU share: OMP_NUM_THREADS (the pool sets it to the
+    share) caps the workers, never above the CPUs this process may run on; the report keeps
+    the whole machine's nproc next to it (for the full-host estimate)."""
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    hc = bench.host_cpu()
+    assert 1 <= hc["threads"] <= 3 and hc["threads"] <= hc["affinity"]
+    assert hc["nproc"] == os.cpu_count() and hc["omp_num_threads"] == "3"
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    hc = bench.host_cpu()
+    assert hc["threads"] <= hc["affinity"] and hc["omp_num_threads"] is None
+    q = bench.cgroup_cpus()
+    if q is not None:
+        assert hc["threads"] <= max(1, int(q))
