@@ -450,10 +450,6 @@ sim_kernel(const SimArgs *Ap) {
 
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
-    /* FF: the chunk after nxt, loaded when the group enters fast-forward mode and at each
-     * crossing, one step before a crossing needs it (the hit runs of a C4 tail cross a chunk
-     * every step, so a load issued at the crossing itself was waited for at the next step) */
-    uint4 nx2 = make_uint4(0, 0, 0, 0);
     uint64_t sys = 0;
     /* this node's trace slot, set when a system starts (measured: recomputing it at each
      * refill costs more than the two VGPRs) */
@@ -659,10 +655,10 @@ sim_kernel(const SimArgs *Ap) {
     #pragma unroll
                             for (int q = 0; q < 4; ++q) X[q] = cross ? nxt[q] : cur[q];
                             ff_shift(X, cross ? k - m : k, cur);
-                            if (cross) {   /* nxt from nx2; the chunk after that in flight */
-                                nxt[0] = nx2.x; nxt[1] = nx2.y; nxt[2] = nx2.z; nxt[3] = nx2.w;
-                                const uint32_t pc = ((nd.ip >> 3) + 3) * 8u;
-                                nx2 = ld16(tb + (pc + 8u <= stride ? pc : stride - 8u));
+                            if (cross) {   /* the chunk after: used next iteration at the earliest */
+                                const uint32_t pc = ((nd.ip >> 3) + 2) * 8u;
+                                const uint4 v = ld16(tb + (pc + 8u <= stride ? pc : stride - 8u));
+                                nxt[0] = v.x; nxt[1] = v.y; nxt[2] = v.z; nxt[3] = v.w;
                             }
                         }
                         nd.ip += k;
@@ -991,10 +987,6 @@ sim_kernel(const SimArgs *Ap) {
         const uint64_t enter = ((one << NP) - one) & ~ffm;
         ffm |= enter;
         ffip = __builtin_amdgcn_inverse_ballot_w64(enter) ? nd.ip : ffip;   /* segment start */
-        if (!GEN && __builtin_amdgcn_inverse_ballot_w64(enter)) {
-            const uint32_t pc = ((nd.ip >> 3) + 2) * 8u;                  /* the chunk after nxt */
-            nx2 = ld16(tb + (pc + 8u <= stride ? pc : stride - 8u));
-        }
         pint = one ? FF_PROBE : (pint < FF_PROBE_MAX ? 2u * pint : FF_PROBE_MAX);
         pcd = pint;
     };
