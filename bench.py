@@ -58,13 +58,7 @@ def shard(rank, n_per_rank):
 def reduce_counters(vec, dist_mod=None):
     """All-reduce a 32-entry uint64 counter vector across ranks: sums (mod 2^64) for every
     slot except max_rounds (slot 24), which is a max.  `vec` is a torch int64 tensor."""
-    if dist_mod is None or not dist_mod.is_initialized():
-        return vec
-    mx = vec[24:25].clone()
-    dist_mod.all_reduce(vec, op=dist_mod.ReduceOp.SUM)
-    dist_mod.all_reduce(mx, op=dist_mod.ReduceOp.MAX)
-    vec[24:25] = mx
-    return vec
+    return reduce_vector(vec, dist_mod, (24,))
 
 
 def launch_ranks(n, argv, cmd=None, timeout=None):
@@ -195,14 +189,126 @@ def cpu_baseline_reference(dist, n_instr, seed, n_sample, procs):
                        f"{t:.2f} s (generation and initializeProcessor untimed)")
 
 
-def golden_aggregate(config):
-    """The full-size golden aggregate of a bench workload (oracle/gen_fixtures.py aggregates:
-    the reference's handler text over every system), or None."""
+DIST_CODE = {"uniform": 0, "hot": 1, "evict": 2}
+GOLDEN = os.path.join(REPO, "tests", "golden")
+# the aggregate of a system range as a vector (all-reduced across ranks: sums mod 2^64, a max
+# for max_rounds) followed by the per-rank shard verdicts (ranks whose shard equals its
+# reference aggregate / differs / has none)
+AGG_VEC = ("systems", "msgs", "instrs", "rounds", "max_rounds", "st0", "st1", "st2", "st3", "st4",
+           "sum_dump_hash", "sum_final_hash", "result_digest", "shards_ok", "shards_bad",
+           "shards_unpinned")
+AGG_MAX = AGG_VEC.index("max_rounds")
+
+
+def _load_json(p):
     try:
-        with open(os.path.join(REPO, "tests", "golden", "aggregates.json")) as f:
-            return json.load(f).get(config)
+        with open(p) as f:
+            return json.load(f)
     except (OSError, ValueError):
-        return None
+        return {}
+
+
+def golden_for(dname, seed, n_instr, first, n):
+    """The reference's aggregate of system ids [first, first + n) of a workload and where it
+    comes from: an entry of tests/golden/aggregates.json over exactly that range (the
+    reference's handler text over every system -- oracle/gen_fixtures.py aggregates / shards:
+    each shard of the 1..8-GPU bench and the job totals at 2/4/8 GPUs), else the aggregate of
+    the slice of a golden per-system fixture (tests/golden/ensemble/np8_*.npy) that holds the
+    range.  (None, None) when nothing pins it."""
+    import pydsm
+    code = DIST_CODE[dname]
+    want = dict(np=NP, dist=code, seed=seed, n_instr=n_instr)
+    for key, g in sorted(_load_json(os.path.join(GOLDEN, "aggregates.json")).items()):
+        if all(g.get(k) == v for k, v in want.items()) and g.get("first_sys") == first \
+                and g.get("systems") == n:
+            return g, "aggregates.json:" + key
+    for key, m in sorted(_load_json(os.path.join(GOLDEN, "ensemble", "meta.json")).items()):
+        if all(m.get(k) == v for k, v in want.items()) and \
+                m["first_sys"] <= first and first + n <= m["first_sys"] + m["n_sys"]:
+            lo = first - m["first_sys"]
+            g = np.load(os.path.join(GOLDEN, "ensemble", key + ".npy"))[lo:lo + n]
+            res = np.zeros(n, dtype=pydsm.RESULT_DTYPE)
+            for i, f in enumerate(("status", "rounds", "msgs", "instrs", "dump_hash",
+                                   "final_hash")):
+                res[f] = g[:, i]
+            return pydsm.aggregate(res, first), f"ensemble/{key}.npy[{lo}:{lo + n}]"
+    return None, None
+
+
+def agg_to_vec(a, verdict=None):
+    """An aggregate dict (+ this rank's shard verdict: 'ok' / 'bad' / 'unpinned') as AGG_VEC."""
+    v = [a["systems"], a["msgs"], a["instrs"], a["rounds"], a["max_rounds"]] + list(a["status"]) + \
+        [int(a[k], 16) for k in ("sum_dump_hash", "sum_final_hash", "result_digest")] + \
+        [int(verdict == "ok"), int(verdict == "bad"), int(verdict == "unpinned")]
+    return np.array([x & 0xFFFFFFFFFFFFFFFF for x in v], dtype=np.uint64)
+
+
+def vec_to_agg(v):
+    v = [int(x) for x in np.asarray(v, dtype=np.uint64)]
+    a = dict(zip(AGG_VEC, v))
+    out = {k: a[k] for k in ("systems", "msgs", "instrs", "rounds", "max_rounds")}
+    out["status"] = [a[f"st{i}"] for i in range(5)]
+    out.update({k: "0x%016x" % a[k] for k in ("sum_dump_hash", "sum_final_hash", "result_digest")})
+    return out, dict(ok=a["shards_ok"], bad=a["shards_bad"], unpinned=a["shards_unpinned"])
+
+
+def reduce_vector(vec, dist_mod, max_slots=()):
+    """All-reduce an int64 torch vector across ranks: sums (mod 2^64) except the `max_slots`."""
+    if dist_mod is None or not dist_mod.is_initialized():
+        return vec
+    mx = [vec[i:i + 1].clone() for i in max_slots]
+    dist_mod.all_reduce(vec, op=dist_mod.ReduceOp.SUM)
+    for i, m in zip(max_slots, mx):
+        dist_mod.all_reduce(m, op=dist_mod.ReduceOp.MAX)
+        vec[i:i + 1] = m
+    return vec
+
+
+def check_aggregate(mine, gold, counters=None):
+    """Differences between an aggregate (and the engine's own counters over the same systems,
+    when given) and the reference's; [] when equal."""
+    import pydsm
+    diff = pydsm.aggregate_diff(mine, gold)
+    if counters is not None:
+        for k in ("msgs", "instrs", "rounds", "systems", "max_rounds"):
+            if counters[k] != gold[k] and k not in diff:
+                diff.append("counter " + k)
+        if counters["sum_final_hash"] != int(gold["sum_final_hash"], 16):
+            diff.append("counter sum_final_hash")
+    return diff
+
+
+def shard_parity(dname, seed, n_instr, first, res_host, counters):
+    """This rank's shard against the reference: ('ok' | 'bad' | 'unpinned', message)."""
+    import pydsm
+    mine = pydsm.aggregate(res_host, first)
+    gold, src = golden_for(dname, seed, n_instr, first, len(res_host))
+    if gold is None:
+        return mine, "unpinned", f"shard [{first}, {first + len(res_host)}): no reference aggregate"
+    diff = check_aggregate(mine, gold, counters)
+    return mine, ("bad" if diff else "ok"), (
+        f"shard [{first}, {first + len(res_host)}) " +
+        (f"== reference ({src})" if not diff else f"MISMATCH vs {src}: " + ",".join(diff)))
+
+
+def job_parity(dname, seed, n_instr, world, n_per_rank, total_vec, counters):
+    """The job's all-reduced aggregate and counters (ids [0, world * n_per_rank)) against the
+    reference, plus the per-shard tally: the bench line's `parity` string."""
+    tot, tally = vec_to_agg(total_vec)
+    gold, src = golden_for(dname, seed, n_instr, 0, world * n_per_rank)
+    if gold is None:
+        job = f"job total over {world} shard(s) unpinned (no reference aggregate for " \
+              f"[0, {world * n_per_rank}))"
+    else:
+        diff = check_aggregate(tot, gold, counters)
+        job = (f"full-size aggregate == reference (job total over {world} shard(s), {src})"
+               if not diff else f"AGGREGATE MISMATCH vs {src}: " + ",".join(diff))
+    shards = f"{tally['ok']}/{world} shards == their reference aggregates"
+    if tally["bad"]:
+        shards += f"; {tally['bad']} SHARD MISMATCH"
+    if tally["unpinned"]:
+        shards += f"; {tally['unpinned']} unpinned"
+    return job + "; " + shards, dict(job_source=src, shards=tally)
 
 
 def traffic_from_profiles(config):
@@ -214,6 +320,12 @@ def traffic_from_profiles(config):
         return e if e else None
     except (OSError, ValueError):
         return None
+
+
+def issue_from_profiles(config):
+    """Per transition kernel: VALU-busy fraction, waves per SIMD, wait / issue-stall fractions,
+    LDS bank conflicts (profiles/pmc_issue.json, tools/issue.py), or None."""
+    return _load_json(os.path.join(REPO, "profiles", "pmc_issue.json")).get(config) or None
 
 
 def main():
@@ -396,6 +508,18 @@ def main():
     tot = reduce_counters(cnt.clone().to(cdev), dist if use_dist else None)
     c = pydsm.counters_to_dict(tot.cpu().numpy().view(np.uint64))
 
+    # parity after the timed region, on every rank: the last step's per-system results of this
+    # rank's shard against the reference's own handler text (its full-size aggregate:
+    # counters, status counts, hash sums, position-sensitive result digest), then the job's
+    # all-reduced aggregate against the reference's total over ids [0, world * n)
+    res_host = out.cpu().numpy().view(pydsm.RESULT_DTYPE).reshape(-1)
+    mine, verdict, shard_msg = shard_parity(dname, seed, n_instr, first, res_host, local_c)
+    print(f"bench.py rank {rank}: {shard_msg}", file=sys.stderr, flush=True)
+    avec = torch.from_numpy(agg_to_vec(mine, verdict).view(np.int64).copy()).to(cdev)
+    avec = reduce_vector(avec, dist if use_dist else None, (AGG_MAX,))
+    parity, parity_detail = job_parity(dname, seed, n_instr, world, n_sys,
+                                       avec.cpu().numpy().view(np.uint64), c)
+
     if rank == 0:
         K = args.steps
         value = c["msgs"] * K / elapsed_max
@@ -437,39 +561,33 @@ def main():
             roof["traffic"] = int(tr["sim_kernel"].get("bytes_per_launch") * launches)
             roof["traffic_source"] = tr["sim_kernel"].get("source") + (
                 " (per-dispatch average x 2 dispatches per step)" if launches == 2 else "")
+        # the compute-side roof of the transition kernels that ran (VALU utilisation,
+        # occupancy, waits, LDS bank conflicts beside the HBM fraction), from the PMC passes
+        # under profiles/ (tools/issue.py -> profiles/pmc_issue.json): these kernels are bound
+        # by a round's dependent instruction chain, not by HBM
+        iss = issue_from_profiles(args.config) or {}
+        ran = ["sim_kernel_budget"] + (["ser_kernel"] if serial else
+                                       ["sim_kernel_ff"] if ff_picked and launches == 2 else [])
+        if not args.fused and all(k in iss for k in ran):
+            roof["issue"] = {k: iss[k] for k in ran}
+            roof["issue_how"] = ("valu_busy = SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); "
+                                 "waves_per_simd = SQ_WAVE_CYCLES x 4 / (GRBM_GUI_ACTIVE / 8) / 1024; "
+                                 "wait_frac / issue_stall_frac = SQ_WAIT_ANY / SQ_WAIT_INST_ANY over "
+                                 "their sum with SQ_ACTIVE_INST_ANY; clock = GRBM_GUI_ACTIVE / 8 / wall")
         for phase, kname in ((trace_parse, "parse_kernel"), (dump_stream, "fmt_kernel"),
                              (trace_stream, "gen_kernel")):
             if phase is not None and tr.get(kname):
                 phase["traffic"] = tr[kname].get("bytes_per_launch")
-        # parity after the timed region: the last step's per-system results against the
-        # reference's own handler text -- the full-size golden aggregates (counters, status
-        # counts, hash sums, per-system result digest; tests/golden/aggregates.json) and the
-        # golden per-system prefix (tests/golden/ensemble/np8_<dist>.npy)
-        parity = None
-        if rank == 0 and first == 0 and not args.systems:
-            res_host = out.cpu().numpy().view(pydsm.RESULT_DTYPE).reshape(-1)
-            gold = golden_aggregate(args.config)
-            checks = []
-            if gold is not None and gold["systems"] == n_sys:
-                mine = pydsm.aggregate(res_host)
-                diff = pydsm.aggregate_diff(mine, gold)
-                for k in ("msgs", "instrs", "rounds", "systems", "max_rounds"):
-                    if local_c[k] != gold[k] and k not in diff:
-                        diff.append("counter " + k)
-                if local_c["sum_final_hash"] != int(gold["sum_final_hash"], 16):
-                    diff.append("counter sum_final_hash")
-                checks.append("full-size aggregate == reference" if not diff else
-                              "AGGREGATE MISMATCH: " + ",".join(diff))
-            gp = os.path.join(REPO, "tests", "golden", "ensemble", f"np8_{dname}.npy")
-            if os.path.exists(gp):
-                g = np.load(gp)
-                r = res_host[:len(g)]
-                mine = np.stack([r["status"].astype(np.uint64), r["rounds"].astype(np.uint64),
-                                 r["msgs"].astype(np.uint64), r["instrs"].astype(np.uint64),
-                                 r["dump_hash"], r["final_hash"]], axis=1)
-                checks.append(f"golden[0:{len(g)}] bit-exact" if np.array_equal(mine, g)
-                              else "GOLDEN MISMATCH")
-            parity = "; ".join(checks) if checks else None
+        # and system by system: the golden per-system prefix (tests/golden/ensemble/np8_<dist>.npy)
+        gp = os.path.join(GOLDEN, "ensemble", f"np8_{dname}.npy")
+        if first == 0 and os.path.exists(gp):
+            g = np.load(gp)
+            r = res_host[:len(g)]
+            mine6 = np.stack([r["status"].astype(np.uint64), r["rounds"].astype(np.uint64),
+                              r["msgs"].astype(np.uint64), r["instrs"].astype(np.uint64),
+                              r["dump_hash"], r["final_hash"]], axis=1)
+            parity += (f"; golden[0:{len(r)}] bit-exact" if np.array_equal(mine6, g[:len(r)])
+                       else "; GOLDEN MISMATCH")
         cpu = cpu_port = None
         if world == 1 and not args.no_cpu:
             hc = host_cpu()
@@ -525,6 +643,7 @@ def main():
             "kernel_ms": [round(x, 3) for x in kms],
             "sum_final_hash": hex(c["sum_final_hash"]),
             "parity": parity,
+            "parity_detail": parity_detail,
             "collective": (("rccl" if backend == "nccl" else backend) + f" all_reduce of 32 counters over {world} rank(s)")
                           if use_dist else None,
             "launch": eng.launch_info(),

@@ -402,8 +402,9 @@ def result_digest(res, first_idx=0):
         return int(h.sum(dtype=np.uint64))
 
 
-def aggregate(res):
-    """The golden-aggregate view of per-system results (gen_fixtures.py aggregates)."""
+def aggregate(res, first_idx=0):
+    """The golden-aggregate view of per-system results (gen_fixtures.py aggregates) of the
+    systems with ids first_idx, first_idx + 1, ..."""
     res = np.ascontiguousarray(res).view(RESULT_DTYPE).reshape(-1)
     st = np.bincount((res["status"] & 0xFF).astype(np.int64), minlength=5)
     with np.errstate(over="ignore"):
@@ -414,7 +415,7 @@ def aggregate(res):
                 "status": [int(x) for x in st[:5]],
                 "sum_dump_hash": "0x%016x" % int(res["dump_hash"].sum(dtype=np.uint64)),
                 "sum_final_hash": "0x%016x" % int(res["final_hash"].sum(dtype=np.uint64)),
-                "result_digest": "0x%016x" % result_digest(res)}
+                "result_digest": "0x%016x" % result_digest(res, first_idx)}
 
 
 AGG_KEYS = ("systems", "msgs", "instrs", "rounds", "max_rounds", "status", "sum_dump_hash",

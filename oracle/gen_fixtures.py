@@ -215,6 +215,71 @@ def aggregates():
             json.dump(out, f, indent=1, sort_keys=True)
 
 
+# multi-GPU bench (weak scaling, bench.shard): rank r simulates ids [r*n, (r+1)*n).  Every
+# shard of an 8-GPU run gets its own reference aggregate ("<config>@<r>"; shard 0 is the
+# "<config>" entry above), and the job totals at 2, 4 and 8 GPUs ("<config>@x<N>") are the
+# merge of shards 0..N-1 -- sums mod 2^64 for the hashes and the position-sensitive digest,
+# max for max_rounds -- which equals one reference run over ids [0, N*n)
+# (tests/test_aggregates.py checks that identity on small ranges).
+SHARDED = {"random": 0, "hot": 1, "evict": 2}
+MAX_RANKS = 8
+M64 = (1 << 64) - 1
+
+
+def merge_aggregates(parts):
+    """The aggregate of a union of disjoint system ranges (ref_lockstep.c agg_merge)."""
+    out = dict(systems=0, msgs=0, instrs=0, rounds=0, max_rounds=0, status=[0] * 5)
+    h = dict(sum_dump_hash=0, sum_final_hash=0, result_digest=0)
+    for p in parts:
+        for k in ("systems", "msgs", "instrs", "rounds"):
+            out[k] += p[k]
+        out["max_rounds"] = max(out["max_rounds"], p["max_rounds"])
+        out["status"] = [a + b for a, b in zip(out["status"], p["status"])]
+        for k in h:
+            h[k] = (h[k] + int(p[k], 16)) & M64
+    out.update({k: "0x%016x" % v for k, v in h.items()})
+    return out
+
+
+def shards():
+    """Reference aggregates of shards 1..7 of every bench workload (shard 0 is aggregates()'s
+    entry) and the 2/4/8-GPU job totals."""
+    p = os.path.join(GOLD, "aggregates.json")
+    out = json.load(open(p))
+    only = os.environ.get("AGG_ONLY")
+    for name, dist in SHARDED.items():
+        if only and name not in only.split(","):
+            continue
+        base = out[name]
+        n, seed, n_instr = base["systems"], base["seed"], base["n_instr"]
+        parts = [base]
+        for r in range(1, MAX_RANKS):
+            key = f"{name}@{r}"
+            d = out.get(key)
+            if d is None or d.get("first_sys") != r * n or d.get("systems") != n:
+                res = subprocess.run([os.path.join(REFBIN, "ref_lockstep_np8"), "agg", str(dist),
+                                      str(seed), str(n_instr), str(r * n), str(n),
+                                      str(os.cpu_count() or 8)],
+                                     check=True, capture_output=True, text=True)
+                d = json.loads(res.stdout.strip().splitlines()[-1])
+                d.update(np=8, dist=dist, seed=seed, n_instr=n_instr, first_sys=r * n,
+                         producer="oracle/_ref/ref_lockstep_np8 agg (assignment.c handler/issue "
+                                  "text, lock-step schedule)")
+                out[key] = d
+                print("  ", key, d["msgs"], d["result_digest"], flush=True)
+                with open(p, "w") as f:
+                    json.dump(out, f, indent=1, sort_keys=True)
+            parts.append(d)
+        for g in (2, 4, 8):
+            t = merge_aggregates(parts[:g])
+            t.update(np=8, dist=dist, seed=seed, n_instr=n_instr, first_sys=0, gpus=g,
+                     producer=f"merge of the reference aggregates of shards 0..{g - 1} "
+                              f"(oracle/gen_fixtures.py shards)")
+            out[f"{name}@x{g}"] = t
+        with open(p, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+
+
 EXPLORE_K, EXPLORE_SEED, EXPLORE_THRESH = 256, 7, 0x8000
 ISSUE_RE = re.compile(rb"^Processor \d+: instr type=.*\n", re.M)
 

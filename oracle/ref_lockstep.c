@@ -386,7 +386,7 @@ int main(int argc, char **argv) {
                     run_system(&res, dump, fin);
                     clock_gettime(CLOCK_MONOTONIC, &tb);
                     a.ns += (uint64_t)(tb.tv_sec - ta.tv_sec) * 1000000000ull + (uint64_t)(tb.tv_nsec - ta.tv_nsec);
-                    agg_add(&a, sy - first, &res);
+                    agg_add(&a, sy, &res);   /* absolute system id: shards merge */
                 }
                 for (int t = 0; t < NUM_PROCS; ++t) {
                     char q[64]; snprintf(q, sizeof q, "tests/empty/core_%d.txt", t); unlink(q);

@@ -56,3 +56,20 @@ def test_rccl_collective_path_one_rank():
     for k in ("msgs", "instrs", "rounds", "systems", "max_rounds", "status_DEADLOCKED"):
         assert rccl["counters"][k] == plain["counters"][k], k
     assert rccl["sum_final_hash"] == plain["sum_final_hash"]
+
+
+@pytest.mark.parametrize("gpus,config,n", [(2, "random", 2048), (4, "evict", 1024)])
+def test_multi_rank_line_checks_every_shard_and_the_total(gpus, config, n):
+    """`--gpus N` (every rank on device 0, gloo): each rank checks its shard's results against
+    the reference's aggregate of its id range, rank 0 the all-reduced job total against the
+    reference's over [0, N * n) -- the bench line's `parity` says both (here the ranges lie in
+    the 4096-system golden fixtures; at full size, tests/golden/aggregates.json's <config>@<r>
+    shard entries and <config>@x<N> totals)."""
+    small = ["--systems", str(n)] + SMALL[2:]
+    line = _bench(["--gpus", str(gpus), "--config", config] + small,
+                  env={"DSM_BENCH_BACKEND": "gloo", "DSM_BENCH_DEVICE": "0"})
+    assert line["n_gpus"] == gpus
+    assert line["parity"].startswith(f"full-size aggregate == reference (job total over {gpus} shard(s)"), line["parity"]
+    assert f"{gpus}/{gpus} shards == their reference aggregates" in line["parity"], line["parity"]
+    assert line["parity_detail"]["shards"] == dict(ok=gpus, bad=0, unpinned=0)
+    assert "golden[0:%d] bit-exact" % n in line["parity"]
