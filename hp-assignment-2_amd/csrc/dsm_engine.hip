@@ -450,6 +450,10 @@ sim_kernel(const SimArgs *Ap) {
 
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
+    /* FF: the line tags for a hit, a byte per line (RD needs a valid line, state != I; WR one
+     * in M or E, state <= E; 0xFF never equals a 7-bit address), set at mode entry: in the
+     * mode no message arrives and a write hit on E leaves M, still a hit for both */
+    uint32_t fkr = 0, fkw = 0;
     uint64_t sys = 0;
     /* this node's trace slot, set when a system starts (measured: recomputing it at each
      * refill costs more than the two VGPRs) */
@@ -539,7 +543,11 @@ sim_kernel(const SimArgs *Ap) {
      * normal round: the last write to each line within [ffip, ip) and the last write overall,
      * found by scanning the instructions back from ip (all of them hits).  Lanes with go. */
     auto ff_settle = [&](bool go) {
-        uint32_t need = (go && nd.ip > ffip) ? 0x1Fu : 0u;    /* lines 0-3, pending (bit 4) */
+        /* lines 0-3 (only those in M or E at mode entry: a write hit needs one, so the other
+         * lines were not written in the segment) and pending (bit 4) */
+        const uint32_t wl = (((fkw & 0xFFu) != 0xFFu) ? 1u : 0u) | (((fkw & 0xFF00u) != 0xFF00u) ? 2u : 0u) |
+                            (((fkw & 0xFF0000u) != 0xFF0000u) ? 4u : 0u) | (((fkw >> 24) != 0xFFu) ? 8u : 0u);
+        uint32_t need = (go && nd.ip > ffip && wl) ? (0x10u | wl) : 0u;
         uint32_t i = nd.ip, lval = 0, wm = 0, pv = 0;
         while (__ballot(need != 0u)) {
             if (need) {
@@ -605,14 +613,8 @@ sim_kernel(const SimArgs *Ap) {
                 if (inff) {
                     const bool iss = (nd.ctl & C_WAIT) == 0u && nd.ip < nd.nins;
                     const bool dpend = (nd.ctl & (C_WAIT | C_DUMPED)) == 0u && nd.ip >= nd.nins;
-                    /* line tags for a hit, a byte per line: RD needs a valid line (state != I),
-                     * WR one in M or E (state <= E); 0xFF never equals a 7-bit address */
-                    const uint32_t L0 = s_line[wv][0][lane], L1 = s_line[wv][1][lane];
-                    const uint32_t L2 = s_line[wv][2][lane], L3 = s_line[wv][3][lane];
-                    const uint32_t la4 = __builtin_amdgcn_perm(L1, L0, 0x0C0C0400u) | __builtin_amdgcn_perm(L3, L2, 0x04000C0Cu);
-                    const uint32_t ls4 = __builtin_amdgcn_perm(L1, L0, 0x0C0C0602u) | __builtin_amdgcn_perm(L3, L2, 0x06020C0Cu);
-                    const uint32_t s_or_i = (ls4 >> 1) & 0x01010101u, inv = ls4 & s_or_i;
-                    const uint32_t kr = la4 | ((inv << 8) - inv), kw = la4 | ((s_or_i << 8) - s_or_i);
+                    /* the hit keys (fkr / fkw), fixed while the group is in the mode */
+                    const uint32_t kr = fkr, kw = fkw;
                     const uint32_t s = nd.ip & 7u, m = 8u - s;
                     uint32_t W[4];
                     if (GEN) {
@@ -987,6 +989,15 @@ sim_kernel(const SimArgs *Ap) {
         const uint64_t enter = ((one << NP) - one) & ~ffm;
         ffm |= enter;
         ffip = __builtin_amdgcn_inverse_ballot_w64(enter) ? nd.ip : ffip;   /* segment start */
+        if (__builtin_amdgcn_inverse_ballot_w64(enter)) {
+            const uint32_t L0 = s_line[wv][0][lane], L1 = s_line[wv][1][lane];
+            const uint32_t L2 = s_line[wv][2][lane], L3 = s_line[wv][3][lane];
+            const uint32_t la4 = __builtin_amdgcn_perm(L1, L0, 0x0C0C0400u) | __builtin_amdgcn_perm(L3, L2, 0x04000C0Cu);
+            const uint32_t ls4 = __builtin_amdgcn_perm(L1, L0, 0x0C0C0602u) | __builtin_amdgcn_perm(L3, L2, 0x06020C0Cu);
+            const uint32_t s_or_i = (ls4 >> 1) & 0x01010101u, inv = ls4 & s_or_i;
+            fkr = la4 | ((inv << 8) - inv);
+            fkw = la4 | ((s_or_i << 8) - s_or_i);
+        }
         pint = one ? FF_PROBE : (pint < FF_PROBE_MAX ? 2u * pint : FF_PROBE_MAX);
         pcd = pint;
     };
@@ -1045,7 +1056,25 @@ sim_kernel(const SimArgs *Ap) {
  * beyond the inbox limit hands the system to the 256-deep re-run, as a ring overflow of the
  * lock-step kernel does.  The issuing node's trace chunk and the next one are kept in
  * registers (refill step below). */
-constexpr int SER_WAVES = 6, SER_RF = 16;
+#ifndef SER_RF_DEF
+#define SER_RF_DEF 8
+#endif
+#ifndef SER_GE_DEF
+#define SER_GE_DEF 1
+#endif
+#ifndef SER_MACRO_DEF
+#define SER_MACRO_DEF 1     /* lone-node macro-steps per iteration (0: off) */
+#endif
+/* SER_RF: iterations between trace refills; SER_GE: the one-action step (ser_step) runs in
+ * every SER_GE-th iteration (the macro-step in every one) */
+constexpr int SER_WAVES = 6, SER_RF = SER_RF_DEF, SER_GE = SER_GE_DEF;
+constexpr int SER_MACRO = SER_MACRO_DEF;   /* lone-node macro-steps per iteration */
+/* SER_PROBE builds (diagnostics, never the default): per-wave event counts of the serial pass
+ * in the counter slots the pass leaves unused (msgs_by_type 0-4): iterations, iterations with
+ * a macro-step, with a one-action step, with a chunk miss, hand-overs */
+#ifndef SER_PROBE
+#define SER_PROBE 0
+#endif
 
 template <int W>
 struct LdsCol {
@@ -1207,6 +1236,7 @@ ser_kernel(const SimArgs *Ap) {
         nxv = nxv & !rot;
         tci = rot ? c : tci;
         if (__ballot(miss)) {            /* another node issues, or a system's first issue */
+            if (SER_PROBE && lane == 0) atomicAdd(&s_cnt[3], 1ull);
             if (miss) {
                 cur = ld16(slot_of(nd) + 8u * c);
                 pfv = nxv = false;
@@ -1268,11 +1298,36 @@ ser_kernel(const SimArgs *Ap) {
 
     bool live = claim();
     uint32_t v = live ? start() : SR_RUN;
-    uint32_t iters = 0;
+    uint32_t iters = 0, nmac = 0;
     for (;;) {
 #pragma unroll 1
         for (int k = 0; k < SER_RF; ++k) {
-            if (live && v == SR_RUN) v = ser_step<NP, S_QN, CAP>(m, r, T, fetch, on_dump, lim_rsh, cap);
+            /* a lone node's whole transaction at once (ser_macro), else one node-action */
+            bool mac = false;
+            if (!CAP) {
+#pragma unroll
+                for (int j = 0; j < SER_MACRO; ++j) {
+                    const bool q = live && v == SR_RUN && ser_quiet_lone(r, lim_rsh) && (j == 0 || mac);
+                    bool did = false;
+                    if (__ballot(q) && q) did = ser_macro<NP>(m, r, fetch);
+                    mac = mac || did;
+                    nmac += did ? 1u : 0u;
+                }
+            }
+            if (SER_PROBE) {
+                const uint64_t gm = __ballot(live && v == SR_RUN && !mac), mm = __ballot(mac);
+                if (lane == 0) {
+                    atomicAdd(&s_cnt[0], 1ull);
+                    if (mm) atomicAdd(&s_cnt[1], 1ull);
+                    if (gm) atomicAdd(&s_cnt[2], 1ull);
+                }
+            }
+            if (live && v == SR_RUN && !mac && (k % SER_GE) == 0)
+                v = ser_step<NP, S_QN, CAP>(m, r, T, fetch, on_dump, lim_rsh, cap);
+            if (SER_PROBE) {
+                const uint64_t hm = __ballot(live && v != SR_RUN);
+                if (lane == 0 && hm) atomicAdd(&s_cnt[4], 1ull);
+            }
             if (live && v != SR_RUN) {
                 finish(v);
                 live = claim();
@@ -1284,6 +1339,7 @@ ser_kernel(const SimArgs *Ap) {
         if (__ballot(live) == 0) break;
     }
     if (lane == 0) atomicAdd(&s_cnt[K_WROUNDS], (unsigned long long)iters);
+    if (!CAP && nmac) atomicAdd(&s_cnt[K_FFPASS], (unsigned long long)nmac);   /* multi-round steps */
     __syncthreads();
     if (threadIdx.x < K_N) {
         const unsigned long long x = s_cnt[threadIdx.x];
@@ -1595,19 +1651,22 @@ extern "C" void dsm_close(dsm_ctx *c) {
 
 extern "C" int dsm_launch_info_get(dsm_ctx *c, dsm_launch_info *info) {
     if (!c || !info) return DSM_E_INVAL;
-    if (c->last_pair && c->last_blog) {
+    if (c->last_pair) {
         /* the trace scan chose the pair's kernel on the device: wait for the run, read the
-         * verdict (ff_verdict) and report the passes that actually ran */
+         * verdict (ff_verdict) and report the passes that actually ran (one pass at budget
+         * 0: only the kernel it picked) */
         uint32_t scan[2] = {0, 0};
         HIPCK(hipSetDevice(c->device));
         HIPCK(hipStreamSynchronize(c->last_st));
         HIPCK(hipMemcpy(scan, c->d_ctrl + CTRL_SCAN, sizeof scan, hipMemcpyDeviceToHost));
         const bool ff = scan[1] != 0u && (uint64_t)scan[1] * 16u >= scan[0];
         c->info.ff_picked = ff ? 1 : 0;
-        c->info.resume_form = ff ? DSM_RESUME_FASTFORWARD
-                                 : (c->last_use_ser ? DSM_RESUME_SERIAL : DSM_RESUME_LOCKSTEP);
-        c->info.resume_blocks = (ff || !c->last_use_ser) ? c->last_grid_fast : c->last_ser_blocks;
-        c->info.budget_rounds = (int)((ff && c->last_thr_ff) ? c->last_thr_ff : 1u << c->last_blog);
+        if (c->last_blog) {
+            c->info.resume_form = ff ? DSM_RESUME_FASTFORWARD
+                                     : (c->last_use_ser ? DSM_RESUME_SERIAL : DSM_RESUME_LOCKSTEP);
+            c->info.resume_blocks = (ff || !c->last_use_ser) ? c->last_grid_fast : c->last_ser_blocks;
+            c->info.budget_rounds = (int)((ff && c->last_thr_ff) ? c->last_thr_ff : 1u << c->last_blog);
+        }
         c->last_pair = 0;
     }
     *info = c->info;
@@ -1645,7 +1704,13 @@ extern "C" int dsm_set_inbox_limit(dsm_ctx *c, uint32_t cap) {
 static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys,
                       const uint16_t *d_traces, const uint32_t *d_counts, uint64_t n_sys,
                       dsm_sys_result *d_results, dsm_counters *d_counters, hipStream_t st) {
-    if (n_sys == 0) return DSM_OK;
+    if (n_sys == 0) {    /* nothing launched: the launch info says so */
+        c->last_pair = 0;
+        c->info.grid_blocks = c->info.block_threads = c->info.resume_blocks = 0;
+        c->info.budget_log2 = c->info.late_log2 = c->info.budget_rounds = c->info.ff_picked = 0;
+        c->info.resume_form = DSM_RESUME_NONE;
+        return DSM_OK;
+    }
     if (n_sys > 0xFFFFFFFFull) return DSM_E_INVAL;
     HIPCK(hipSetDevice(c->device));
     const int np = c->cfg.np, gpw = 64 / np;
@@ -1685,7 +1750,6 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
         if ((rc = ensure(&c->d_susp_list, &c->susp_list_cap, (size_t)n_sys))) return rc;
     }
     if ((rc = ensure(&c->d_recs, &c->recs_cap, (size_t)n_sys * np * 8))) return rc;
-    /* the serial pass's spill FIFOs: S_SPILL words per lane (96 MiB on 256 CUs) */
     /* the serial pass's grid: one workgroup per CU, fewer when the ensemble cannot fill
      * them (at most n_sys systems are suspended); its spill FIFOs: S_SPILL words per lane
      * (96 MiB on 256 CUs, 384 KiB per workgroup) */

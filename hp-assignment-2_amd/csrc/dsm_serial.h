@@ -368,6 +368,133 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
     return SR_RUN;
 }
 
+/* ---- lone-survivor transaction macro-step (round 4) ---------------------------------------
+ * After a few thousand rounds a system is one node issuing while every other node waits for
+ * good (or has dumped), with nothing queued: 97% (C3) / 99% (C5) of the serial pass's
+ * node-actions are that node's whole transactions (tools/analyze_macro.c).  From such a quiet
+ * state the schedule is fixed and short: round 1 the node issues; a hit ends there.  A miss
+ * sends the victim's EVICT_* (:616-618, :742-773) to the victim's home, then the request to
+ * the block's home; in round 2 both are handled (the victim's home first, in the round after
+ * when it is also the block's home: its inbox holds the eviction, then the request); the reply
+ * is handled in the round after the request.  A write hit on SHARED sends UPGRADE (:646-659)
+ * and takes the same three rounds without an eviction.  When the handlers send nothing else
+ * -- the eviction's home sends no upgrade notice (:507-519), the request's home answers the
+ * requester directly (no WRITEBACK_INT / WRITEBACK_INV to another owner, :210-233,
+ * :405-432), and a REPLY_ID names no other sharer (no INV fan-out, :350-362) -- the whole
+ * transaction is applied here at once, straight from its handlers:
+ *   EVICT_MODIFIED :541-561, EVICT_SHARED :498-539 (at the home), READ_REQUEST :188-236,
+ *   WRITE_REQUEST :375-435, UPGRADE :298-328, REPLY_RD :238-247, REPLY_WR :437-449,
+ *   REPLY_ID :330-364,
+ * with `rounds` and `msgs` advanced as the lock-step schedule would.  The two homes' words
+ * are read up front and forwarded when the victim's and the request's blocks share one.
+ * Returns false, changing nothing but the fetch cache, when the system is not in such a state
+ * or the transaction would send anything else; ser_step then takes it one action at a time.
+ * Not used in the CAP build (its per-node inbox counts are not kept here). */
+DSM_HD bool ser_quiet_lone(const SReg &r, uint32_t lim_rsh) {
+    /* nothing queued or spilled, exactly one node may act and it is the only one left in the
+     * round, and the round limit is out of reach of the transaction's <= 4 rounds */
+    return (r.nz | (r.q & 0xFFF8u) | r.spl) == 0u && r.A == r.iss && r.A != 0u && (r.A & (r.A - 1u)) == 0u &&
+           ((r.rounds + 4u) >> lim_rsh) == 0u;
+}
+
+template <int NP, class M, class F>
+DSM_HD bool ser_macro(M &m, SReg &r, F &&fetch) {
+    const uint32_t n = s_ctz(r.A), bit = 1u << n;
+    uint32_t ct = m.ld(S_CT + n);
+    const uint32_t ip = ct >> SC_IP;
+    if (ip >= s_ni(r, n)) return false;                       /* the dump: one action */
+    const uint32_t ins = fetch(n, ip, true);
+    const uint32_t a = (ins >> 8) & 0x7Fu, wr = ins >> 15, val = ins & 0xFFu;
+    const uint32_t h = a >> 4, b = a & 15u, idx = a & 3u, sh8 = 8u * idx;
+    const uint32_t laW = m.ld(S_LA + n), lvW = m.ld(S_LV + n);
+    const uint32_t La = (laW >> sh8) & 0xFFu, Lv = (lvW >> sh8) & 0xFFu;
+    const uint32_t lsh = SC_LS + 2u * idx, Ls = (ct >> lsh) & 3u;          /* M0 E1 S2 I3 */
+    const bool hit = (La == a) & (Ls != 3u);                   /* :608, :635 */
+    const bool upg = hit & (wr != 0u) & (Ls == 2u);            /* write hit on SHARED :646 */
+    const bool miss = !hit;
+    const bool ev = miss & (La != 0xFFu) & (Ls != 3u);         /* :616-618, :670-672 */
+    /* the victim's home vh, block vb; the request's home h, block b (every home < NP: a line
+     * holds an address some request brought in; h is checked) */
+    const uint32_t vh = (La >> 4) & 7u, vb = La & 15u;
+    const uint32_t wV = S_MB + 8u * vh + (vb >> 1), wH = S_MB + 8u * h + (b >> 1);
+    const uint32_t mbV = m.ld(wV), dsV = m.ld(S_DS + vh);
+    uint32_t mbH = m.ld(wH), dsH = m.ld(S_DS + h);
+    bool ok = (NP == 8) || (h < (uint32_t)NP);
+    /* the eviction at the victim's home (:498-561); nothing is sent but the upgrade notice */
+    const uint32_t hv = 16u * (vb & 1u), sv = 2u * vb;
+    const uint32_t memV = (mbV >> hv) & 0xFFu, bvV = (mbV >> (hv + 8u)) & 0xFFu, dV = (dsV >> sv) & 3u;
+    const bool mod = Ls == 0u;
+    const bool had = (bvV & bit) != 0u;
+    const uint32_t bvS = bvV & ~bit;                            /* EVICT_SHARED, bit set */
+    const uint32_t rem = (uint32_t)__builtin_popcount(bvS);
+    ok = ok & !(ev & !mod & had & (rem == 1u) & (dV == 1u));   /* S -> EM: notice (:507-519) */
+    uint32_t nbvV = bvV, ndV = dV, nmemV = memV;
+    if (mod) {                                                 /* EVICT_MODIFIED :544-547 */
+        nmemV = Lv;
+        const bool clr = (dV == 0u) & had;
+        nbvV = clr ? 0u : bvV;
+        ndV = clr ? 2u : dV;
+    } else if (had) {                                          /* EVICT_SHARED :501-508 */
+        nbvV = bvS;
+        ndV = rem == 0u ? 2u : dV;
+    }
+    const uint32_t mbV2 = (mbV & ~(0xFFFFu << hv)) | ((nmemV | (nbvV << 8)) << hv);
+    const uint32_t dsV2 = (dsV & ~(3u << sv)) | (ndV << sv);
+    /* the request's home sees the eviction's effect when they share a word */
+    mbH = (ev & (wV == wH)) ? mbV2 : mbH;
+    dsH = (ev & (vh == h)) ? dsV2 : dsH;
+    const uint32_t hh = 16u * (b & 1u), shb = 2u * b;
+    const uint32_t memH = (mbH >> hh) & 0xFFu, bvH = (mbH >> (hh + 8u)) & 0xFFu, dH = (dsH >> shb) & 3u;
+    const uint32_t owner = s_ctz(bvH | 0x100u);                 /* findOwner :98-105 */
+    const uint32_t others = bvH & ~bit;
+    /* EM at another owner: a forward (:222-232, :420-431); S with other sharers on a write or
+     * an upgrade: INV fan-out after REPLY_ID (:350-362); EM with no bit: the reference's
+     * assert (never reached, DESIGN) */
+    const bool em_other = (dH == 0u) & (owner != n);
+    const bool fan = (dH == 1u) & (others != 0u) & ((wr != 0u) | upg);
+    ok = ok & !(miss & em_other) & !((miss | upg) & fan);
+    if (!ok) return false;
+    /* the home's directory entry and memory after the request (:188-236, :298-328, :375-435) */
+    uint32_t nmemH = memH, nbvH = bvH, ndH = dH;
+    bool excl = true;                                          /* REPLY_RD's bitVector == 2 */
+    if (miss & (wr == 0u)) {                                    /* READ_REQUEST */
+        excl = dH != 1u;
+        nbvH = dH == 2u ? bit : (dH == 1u ? (bvH | bit) : bvH);
+        ndH = dH == 2u ? 0u : dH;
+    } else if (miss | upg) {                                    /* WRITE_REQUEST / UPGRADE */
+        nmemH = miss ? val : memH;
+        const bool keep = miss & (dH == 0u);                    /* EM at the requester */
+        nbvH = keep ? bvH : bit;
+        ndH = 0u;
+    }
+    if (miss | upg) {
+        m.st(S_DS + h, (dsH & ~(3u << shb)) | (ndH << shb));
+        m.st(wH, (mbH & ~(0xFFFFu << hh)) | ((nmemH | (nbvH << 8)) << hh));
+    }
+    if (ev) {   /* after the home's write when they share a word: that write holds both */
+        if (vh != h) m.st(S_DS + vh, dsV2);
+        if (wV != wH) m.st(wV, mbV2);
+    }
+    /* the requester's line (:243-246, :445-447, :334-336; a write hit :642-643, :656-657),
+     * pendingWriteValue (:633), the instruction index */
+    const uint32_t nLv = wr ? val : (miss ? memH : Lv);
+    const uint32_t nLs = wr ? 0u : (miss ? (excl ? 1u : 2u) : Ls);
+    m.st(S_LA + n, (laW & ~(0xFFu << sh8)) | (a << sh8));
+    m.st(S_LV + n, (lvW & ~(0xFFu << sh8)) | (nLv << sh8));
+    ct = (ct & ~(3u << lsh)) | (nLs << lsh);
+    ct = wr ? ((ct & ~0xFFu) | val) : ct;
+    m.st(S_CT + n, ct + (1u << SC_IP));
+    /* rounds: the issue, the handling round(s) -- two when the eviction and the request
+     * queue at the same home -- and the reply; messages handled: eviction, request, reply */
+    const bool lone = hit & !upg, twice = ev & (vh == h);
+    const uint32_t R = lone ? 1u : (twice ? 4u : 3u);
+    const uint32_t Mm = lone ? 0u : (ev ? 3u : 2u);
+    r.rounds += R;
+    r.msgs += Mm;
+    r.E = 0u;
+    return true;
+}
+
 /* word i of node n's canonical 64-byte record (dsm_node_state); flags = wait | dumped << 1 */
 template <class M>
 DSM_HD uint32_t ser_rec_word(M &m, uint32_t n, uint32_t flags, int i) {

@@ -268,6 +268,9 @@ DEVI uint32_t lowmask(uint32_t n) { return n >= 32u ? 0xFFFFFFFFu : (1u << n) - 
 #ifndef PARSE_OCC
 #define PARSE_OCC 6
 #endif
+#ifndef PARSE_UNROLL
+#define PARSE_UNROLL 0      /* the chunk loop's first 4 chunks per lane in two fixed rounds */
+#endif
 template <uint32_t BPL>
 __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PARSE_OCC))) parse_kernel(const uint8_t *text, const uint64_t *off,
                                                       uint64_t n_files, uint32_t cap,
@@ -362,6 +365,42 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
              * an address whose home is >= np) are marked in `slow` and scanned exactly after
              * the loop -- inside it, the rare branch's code and registers slowed every round */
             uint32_t mcs = cs, t = isum - nc, slow = 0;
+#if PARSE_UNROLL
+            /* a canonical line is >= 8 bytes, so at most 4 chunks start in a lane's 32 bytes:
+             * two fixed rounds of two independent chunks (their LDS reads issued together, no
+             * ballot or branch between them), then the rest, if any, in the loop below */
+            auto chunk_at = [&](uint32_t b, uint32_t &c0, uint32_t &c1, uint32_t &c2) {
+                const uint32_t o = BPL * lane + b;
+                const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
+                const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
+                c0 = __builtin_amdgcn_alignbyte(d1, d0, o & 3u);
+                c1 = __builtin_amdgcn_alignbyte(d2, d1, o & 3u);
+                c2 = __builtin_amdgcn_alignbyte(d3, d2, o & 3u);
+            };
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                const bool ea = (mcs != 0u) & (t < tmax);
+                const uint32_t ba = (uint32_t)__builtin_ctz(mcs | 0x80000000u);
+                mcs &= mcs - 1u;
+                const bool eb = (mcs != 0u) & (t + 1u < tmax);
+                const uint32_t bb = (uint32_t)__builtin_ctz(mcs | 0x80000000u);
+                mcs &= mcs - 1u;
+                uint32_t a0, a1, a2, b0_, b1_, b2_;
+                chunk_at(ba, a0, a1, a2);
+                chunk_at(bb, b0_, b1_, b2_);
+                const uint32_t oa = BPL * lane + ba, ob = BPL * lane + bb;
+                const uint32_t la = rem - oa < DP_CHUNK ? rem - oa : DP_CHUNK;
+                const uint32_t lb = rem - ob < DP_CHUNK ? rem - ob : DP_CHUNK;
+                uint32_t pa = 0, pb = 0;
+                const bool oka = parse_fast(a0, a1, a2, la, &pa) & (((pa >> 12) & 7u) < (uint32_t)np);
+                const bool okb = parse_fast(b0_, b1_, b2_, lb, &pb) & (((pb >> 12) & 7u) < (uint32_t)np);
+                if (ea & oka) out[idx0 + t] = (uint16_t)pa;
+                if (eb & okb) out[idx0 + t + 1u] = (uint16_t)pb;
+                slow |= (ea & !oka) ? 1u << ba : 0u;
+                slow |= (eb & !okb) ? 1u << bb : 0u;
+                t += 2u;
+            }
+#endif
             while (__ballot((mcs != 0u) & (t < tmax))) {
                 if ((mcs != 0u) & (t < tmax)) {
                     const uint32_t b = (uint32_t)__builtin_ctz(mcs), o = BPL * lane + b;

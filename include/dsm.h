@@ -148,7 +148,9 @@ typedef struct dsm_counters {
     uint64_t overflow_reruns;  /* systems re-run with the 256-deep inbox */
     uint64_t wave_rounds;      /* lock-step loop iterations summed over waves (cost model) */
     uint64_t resumed;          /* systems the two-pass schedule suspended and resumed      */
-    uint64_t ff_passes;        /* hit-run fast-forward steps of a system that advanced it   */
+    uint64_t ff_passes;        /* multi-round steps that advanced a system: hit-run fast-
+                                * forward steps (lock-step kernels) and lone-node transaction
+                                * steps (serial resume pass, dsm_serial.h ser_macro)         */
     uint64_t ff_steps;         /* fast-forward steps per wave (cost model)                  */
     uint64_t ff_sample_instrs; /* DSM_FF_AUTO: instructions of the sampled traces           */
     uint64_t ff_sample_runs;   /* ... of them ending a run of 8 hits (a private 4-line model) */

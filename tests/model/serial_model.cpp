@@ -53,7 +53,7 @@ void to_rec(HostCol &m, uint32_t n, uint32_t flags, dsm_rec *out) {
 }
 
 template <int NP, uint32_t Q>
-int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t cap) {
+int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t cap, bool macro) {
     static uint32_t tab[DT_TABLE_WORDS];
     if (dt_build(tab) > DT_ENTRIES) return 2;
     const HostTab T{tab};
@@ -80,7 +80,7 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
     const uint32_t lim = lim_log2 ? lim_log2 : 22;
     uint64_t compared = 0, ovf = 0, by_status[5] = {0, 0, 0, 0, 0};
     std::vector<uint32_t> col(dsms::S_WORDS), spill(dsms::S_SPILL);
-    uint64_t spilled = 0;
+    uint64_t spilled = 0, n_macro = 0;
     for (uint64_t s = 0; s < n_sys; ++s) {
         HostCol m{col.data(), spill.data()};
         dsms::SReg r;
@@ -93,6 +93,12 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         uint32_t v;
         bool sp = false;
         do {
+            /* as the kernel: a lone node's whole transaction at once when it applies */
+            if (macro && cap >= 256u && dsms::ser_quiet_lone(r, lim) && dsms::ser_macro<NP>(m, r, fetch)) {
+                ++n_macro;
+                v = dsms::SR_RUN;
+                continue;
+            }
             v = cap < 256u ? dsms::ser_step<NP, Q, true>(m, r, T, fetch, on_dump, lim, cap)
                            : dsms::ser_step<NP, Q, false>(m, r, T, fetch, on_dump, lim, cap);
             sp = sp || dsms::s_sq(r.q) != 0u;
@@ -132,9 +138,9 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         ++compared;
         ++by_status[r.st];
     }
-    printf("{\"systems\": %llu, \"compared\": %llu, \"ovf\": %llu, \"spilled\": %llu, \"by_status\": [%llu, %llu, %llu, %llu, %llu]}\n",
+    printf("{\"systems\": %llu, \"compared\": %llu, \"ovf\": %llu, \"spilled\": %llu, \"macro\": %llu, \"by_status\": [%llu, %llu, %llu, %llu, %llu]}\n",
            (unsigned long long)n_sys, (unsigned long long)compared, (unsigned long long)ovf,
-           (unsigned long long)spilled,
+           (unsigned long long)spilled, (unsigned long long)n_macro,
            (unsigned long long)by_status[0], (unsigned long long)by_status[1],
            (unsigned long long)by_status[2], (unsigned long long)by_status[3],
            (unsigned long long)by_status[4]);
@@ -149,14 +155,15 @@ int main(int argc, char **argv) {
     const uint64_t n = strtoull(argv[3], nullptr, 10);
     const uint32_t lim = (uint32_t)atoi(argv[5]), ni = (uint32_t)atoi(argv[6]);
     const uint32_t cap = argc > 7 ? (uint32_t)atoi(argv[7]) : 256u;
-    if (np == 8 && D == 8) return run<8, 8>(dist, n, lim, ni, cap);
-    if (np == 8 && D == 4) return run<8, 4>(dist, n, lim, ni, cap);
-    if (np == 8 && D == 2) return run<8, 2>(dist, n, lim, ni, cap);
-    if (np == 8 && D == 1) return run<8, 1>(dist, n, lim, ni, cap);
-    if (np == 4 && D == 8) return run<4, 8>(dist, n, lim, ni, cap);
-    if (np == 4 && D == 4) return run<4, 4>(dist, n, lim, ni, cap);
-    if (np == 4 && D == 2) return run<4, 2>(dist, n, lim, ni, cap);
-    if (np == 4 && D == 1) return run<4, 1>(dist, n, lim, ni, cap);
+    const bool macro = argc > 8 ? atoi(argv[8]) != 0 : true;   /* ser_macro on (default) */
+    if (np == 8 && D == 8) return run<8, 8>(dist, n, lim, ni, cap, macro);
+    if (np == 8 && D == 4) return run<8, 4>(dist, n, lim, ni, cap, macro);
+    if (np == 8 && D == 2) return run<8, 2>(dist, n, lim, ni, cap, macro);
+    if (np == 8 && D == 1) return run<8, 1>(dist, n, lim, ni, cap, macro);
+    if (np == 4 && D == 8) return run<4, 8>(dist, n, lim, ni, cap, macro);
+    if (np == 4 && D == 4) return run<4, 4>(dist, n, lim, ni, cap, macro);
+    if (np == 4 && D == 2) return run<4, 2>(dist, n, lim, ni, cap, macro);
+    if (np == 4 && D == 1) return run<4, 1>(dist, n, lim, ni, cap, macro);
     fprintf(stderr, "serial_model: no build for np %d, Q %d\n", np, D);
     return 2;
 }

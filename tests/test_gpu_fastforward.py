@@ -148,7 +148,9 @@ def test_fast_forward_modes_agree(dsm, orc, dist):
             out[m] = eng.run_packed(tr, cn)
             _cmp(out[m][0], ores)
     off, on, auto = out[dsm.FF_OFF][1], out[dsm.FF_ON][1], out[dsm.FF_AUTO][1]
-    assert off["ff_passes"] == 0 and off["ff_steps"] == 0 and off["ff_sample_instrs"] == 0
+    # off: no fast-forward step ran (ff_passes may count the serial pass's lone-node
+    # transaction steps, dsm_serial.h ser_macro: multi-round steps too)
+    assert off["ff_steps"] == 0 and off["ff_sample_instrs"] == 0
     assert on["ff_sample_instrs"] == 0
     assert auto["ff_sample_instrs"] == min(n, 4096) * 8 * 256
     picked = auto["ff_sample_runs"] * 16 >= auto["ff_sample_instrs"] and auto["ff_sample_runs"] > 0
@@ -156,3 +158,23 @@ def test_fast_forward_modes_agree(dsm, orc, dist):
     assert (auto["ff_steps"] > 0) == picked
     if dist == "hot":
         assert on["ff_passes"] > 0 and auto["ff_passes"] > 0
+
+
+@pytest.mark.parametrize("dist,picked", [("hot", 1), ("uniform", 0)])
+def test_one_pass_pair_reports_the_kernel_that_ran(dsm, orc, dist, picked):
+    """Budget 0 (one pass) with the automatic fast-forward pair: the launch info reads the trace
+    scan's verdict back, so `ff_picked` names the kernel that ran, not the host's guess; an
+    empty call afterwards reports nothing launched."""
+    n = 2048
+    tr, cn = orc.generate(8, dist, 3, 4096, 0, n)
+    with dsm.Engine(8, 4096) as eng:
+        eng.set_budget(0, 0)
+        res, _ = eng.run_packed(tr, cn)
+        info = eng.launch_info()
+        assert info["ff_picked"] == picked and info["resume_form"] == 0, info
+        assert info["budget_log2"] == 0 and info["budget_rounds"] == 0, info
+        eng.run_packed(tr[:0], cn[:0])
+        info = eng.launch_info()
+        assert info["grid_blocks"] == 0 and info["ff_picked"] == 0 and info["resume_form"] == 0, info
+    ores, _ = orc.run_packed(8, tr, cn, nthreads=16)
+    _cmp(res, ores)

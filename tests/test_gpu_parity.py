@@ -234,6 +234,9 @@ def test_full_size_1m_random(dsm, orc):
     assert cd["sum_final_hash"] == int(ores["final_hash"].sum(dtype=np.uint64))
     assert cd["sum_dump_hash"] == int(ores["dump_hash"].sum(dtype=np.uint64))
     assert cd["msgs"] == int(ores["msgs"].sum()) and cd["instrs"] == int(ores["instrs"].sum())
+    # no system fell off the serial pass's queue + spill to the 256-deep re-run (exact either
+    # way, but a performance cliff)
+    assert cd["overflow_reruns"] == 0
     # golden prefix / suffix pinned by the reference handler text
     _cmp(res[:4096], golden_ensemble("np8_uniform"))
     _cmp(res[999_000:1_000_024], golden_ensemble("np8_uniform_far"))
@@ -269,6 +272,7 @@ def test_full_size_c4_c5(dsm, orc, dist, n):
     assert cd["sum_dump_hash"] == int(ores["dump_hash"].sum(dtype=np.uint64))
     assert cd["msgs"] == int(ores["msgs"].sum()) and cd["instrs"] == int(ores["instrs"].sum())
     assert cd["rounds"] == int(ores["rounds"].sum())
+    assert cd["overflow_reruns"] == 0          # none handed to the 256-deep re-run
     # full-size aggregates of the reference's handler text (every system, result digest)
     assert dsm.aggregate_diff(dsm.aggregate(res), golden_aggregate(dist)) == []
 

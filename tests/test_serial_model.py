@@ -3,7 +3,9 @@ pass's per-lane engine) on the host, whole systems from their first round, again
 oracle (tests/model/serial_model.cpp): results, rounds, records (as hashes) bit-exact,
 including queues that outgrow their slots and continue in the spill FIFO (taken out of order
 when a node's whole inbox is spilled, refilled into the slots in order); under an inbox limit
-the systems that would exceed it are counted (the kernel hands them to the 256-deep re-run)."""
+the systems that would exceed it are counted (the kernel hands them to the 256-deep re-run).
+A lone node's whole transactions are applied at once from a quiet state (ser_macro, as in the
+kernel); two cases run ser_step alone."""
 import json
 import os
 import subprocess
@@ -38,10 +40,13 @@ CASES = [(8, 0, 1500, 8, 0, 4096, 256), (8, 1, 600, 8, 0, 4096, 256),
          (8, 0, 1000, 1, 0, 4096, 256), (4, 0, 1000, 1, 0, 4096, 256),
          (8, 1, 400, 2, 0, 4096, 256), (4, 0, 2000, 2, 0, 4096, 256),
          (4, 3, 1000, 2, 0, 256, 256), (8, 0, 800, 2, 9, 4096, 256), (4, 1, 500, 4, 8, 4096, 256),
-         (8, 0, 1000, 2, 0, 4096, 5), (8, 0, 1000, 8, 0, 4096, 3)]
+         (8, 0, 1000, 2, 0, 4096, 5), (8, 0, 1000, 8, 0, 4096, 3),
+         # the lone-node transaction macro-step (dsm_serial.h ser_macro) off: ser_step alone
+         (8, 0, 1500, 8, 0, 4096, 256, 0), (8, 2, 1000, 2, 0, 4096, 256, 0)]
 
 
-@pytest.mark.parametrize("case", CASES, ids=[f"np{c[0]}_d{c[1]}_D{c[3]}_lim{c[4]}_cap{c[6]}" for c in CASES])
+@pytest.mark.parametrize("case", CASES, ids=[f"np{c[0]}_d{c[1]}_D{c[3]}_lim{c[4]}_cap{c[6]}"
+                                             f"{'_nomacro' if len(c) > 7 and not c[7] else ''}" for c in CASES])
 def test_serial_engine_matches_oracle(serial_model, case):
     r = subprocess.run([serial_model] + [str(x) for x in case], capture_output=True, text=True,
                        timeout=300)
@@ -58,3 +63,9 @@ def test_serial_engine_matches_oracle(serial_model, case):
         assert d["by_status"][3] > 0
     if case[4]:
         assert d["by_status"][4] > 0
+    # the macro-step carries the lone-node tails (never in the CAP build), or is off
+    macro = case[6] == 256 and (len(case) < 8 or case[7])
+    if macro and case[1] in (0, 2) and case[5] == 4096:
+        assert d["macro"] > (100 * d["systems"] if case[4] == 0 else 0), d
+    elif not macro:
+        assert d["macro"] == 0

@@ -47,8 +47,12 @@ for r in range(reps):
         ref = ref or key
         assert key == ref, (v, key, ref)
         res[v].append(ms)
+        if raw[:5].any():       # SER_PROBE builds: serial-pass event counts per wave
+            print(f"{v}: probe iterations {int(raw[0])} macro {int(raw[1])} one-action {int(raw[2])} "
+                  f"chunk-miss {int(raw[3])} hand-over {int(raw[4])} wave_rounds {int(raw[26])}", flush=True)
         info[v] = eng.launch_info()
 for v in variants:
     print(f"{var}={v} [{dist}, {n} systems]: kernel ms median {np.median(res[v]):.2f} "
           f"min {min(res[v]):.2f}  transactions/s {ref[0] / (np.median(res[v]) * 1e-3):.3e}  "
+          f"msgs {ref[0]} final_hash {ref[1]:#x} ff_passes {c['ff_passes']}  "
           f"launch {info[v]}", flush=True)
