@@ -1146,6 +1146,8 @@ ser_kernel(const SimArgs *Ap) {
     unsigned int *const ovf_count = Ap->ovf_count, *const claim_ctr = Ap->claim;
 
     SReg r;
+    SCache cc;                      /* the lone node's words between macro-steps */
+    ser_cache_clear(cc);
     uint64_t sys = 0;
     /* trace chunks of the node that issues (one at a time, almost always the same node):
      * cur = chunk tci of node tn, nx = chunk tci + 1 when nxv, pf = chunk pfc in flight.
@@ -1205,6 +1207,7 @@ ser_kernel(const SimArgs *Ap) {
         }
         r.E = r.nz;
         r.A = r.nz | r.iss;
+        ser_cache_clear(cc);
         tn = 0xFFu;
         nxv = pfv = false;
         if (r.A == 0u) {
@@ -1255,6 +1258,25 @@ ser_kernel(const SimArgs *Ap) {
         const uint32_t wd = (lo & ~m4) | (hi & m4);
         return (wd >> (16u * (j & 1u))) & 0xFFFFu;
     };
+    /* the macro-step's fetch: only from the chunks held in registers (cur, or nx by a
+     * rotation), never a load -- a load here would put its wait (vmcnt(0)) on the main path,
+     * where it also waits for the refill's prefetches and the record stores */
+    auto fetch_reg = [&](uint32_t nd, uint32_t ip, uint32_t &ins) -> bool {
+        const uint32_t c = ip >> 3;
+        const bool tnd = tn == nd;
+        const bool rot = tnd & (tci + 1u == c) & nxv;
+        const bool have = tnd & ((tci == c) | rot);
+        cur.x = rot ? nx.x : cur.x; cur.y = rot ? nx.y : cur.y;
+        cur.z = rot ? nx.z : cur.z; cur.w = rot ? nx.w : cur.w;
+        nxv = nxv & !rot;
+        tci = rot ? c : tci;
+        const uint32_t j = ip & 7u;
+        const uint32_t m2 = 0u - ((j >> 1) & 1u), m4 = 0u - ((j >> 2) & 1u);
+        const uint32_t lo = (cur.x & ~m2) | (cur.y & m2), hi = (cur.z & ~m2) | (cur.w & m2);
+        const uint32_t wd = (lo & ~m4) | (hi & m4);
+        ins = (wd >> (16u * (j & 1u))) & 0xFFFFu;
+        return have;
+    };
     auto refill = [&]() {
         /* pf (chunk pfc, issued at an earlier refill) becomes nx once cur reaches pfc - 1;
          * then the chunk after the newest one held or in flight is requested, so two chunks
@@ -1304,12 +1326,14 @@ ser_kernel(const SimArgs *Ap) {
         for (int k = 0; k < SER_RF; ++k) {
             /* a lone node's whole transaction at once (ser_macro), else one node-action */
             bool mac = false;
+            uint64_t tp0 = 0, tp1 = 0, tp2 = 0;
+            if (SER_PROBE >= 2) tp0 = __builtin_amdgcn_s_memtime();
             if (!CAP) {
 #pragma unroll
                 for (int j = 0; j < SER_MACRO; ++j) {
                     const bool q = live && v == SR_RUN && ser_quiet_lone(r, lim_rsh) && (j == 0 || mac);
                     bool did = false;
-                    if (__ballot(q) && q) did = ser_macro<NP>(m, r, fetch);
+                    if (__ballot(q) && q) did = ser_macro<NP>(m, r, cc, fetch_reg);
                     mac = mac || did;
                     nmac += did ? 1u : 0u;
                 }
@@ -1322,8 +1346,12 @@ ser_kernel(const SimArgs *Ap) {
                     if (gm) atomicAdd(&s_cnt[2], 1ull);
                 }
             }
-            if (live && v == SR_RUN && !mac && (k % SER_GE) == 0)
+            if (SER_PROBE >= 2) tp1 = __builtin_amdgcn_s_memtime();
+            if (live && v == SR_RUN && !mac && (k % SER_GE) == 0) {
                 v = ser_step<NP, S_QN, CAP>(m, r, T, fetch, on_dump, lim_rsh, cap);
+                ser_cache_clear(cc);
+            }
+            if (SER_PROBE >= 2) tp2 = __builtin_amdgcn_s_memtime();
             if (SER_PROBE) {
                 const uint64_t hm = __ballot(live && v != SR_RUN);
                 if (lane == 0 && hm) atomicAdd(&s_cnt[4], 1ull);
@@ -1333,8 +1361,17 @@ ser_kernel(const SimArgs *Ap) {
                 live = claim();
                 v = live ? start() : SR_RUN;
             }
+            if (SER_PROBE >= 2 && lane == 0) {   /* cycles: macro phase, one-action phase, hand-over */
+                const uint64_t tp3 = __builtin_amdgcn_s_memtime();
+                atomicAdd(&s_cnt[5], tp1 - tp0);
+                atomicAdd(&s_cnt[6], tp2 - tp1);
+                atomicAdd(&s_cnt[7], tp3 - tp2);
+            }
         }
+        uint64_t tr0 = 0;
+        if (SER_PROBE >= 2) tr0 = __builtin_amdgcn_s_memtime();
         refill();
+        if (SER_PROBE >= 2 && lane == 0) atomicAdd(&s_cnt[8], __builtin_amdgcn_s_memtime() - tr0);
         iters += SER_RF;
         if (__ballot(live) == 0) break;
     }

@@ -387,6 +387,8 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
  *   REPLY_ID :330-364,
  * with `rounds` and `msgs` advanced as the lock-step schedule would.  The two homes' words
  * are read up front and forwarded when the victim's and the request's blocks share one.
+ * fetch(node, index, &ins) -> false when the instruction is not at hand without a memory
+ * load (the kernel's register-held trace chunks; ser_step then takes the issue and loads it).
  * Returns false, changing nothing but the fetch cache, when the system is not in such a state
  * or the transaction would send anything else; ser_step then takes it one action at a time.
  * Not used in the CAP build (its per-node inbox counts are not kept here). */
@@ -397,16 +399,26 @@ DSM_HD bool ser_quiet_lone(const SReg &r, uint32_t lim_rsh) {
            ((r.rounds + 4u) >> lim_rsh) == 0u;
 }
 
+/* the lone node's own words (control, line addresses, line values) held in registers
+ * between macro-steps: only the node's own actions write them, and a macro-step is the only
+ * action of a system between two of them (ser_step or a hand-over invalidates the cache) */
+struct SCache {
+    uint32_t ct, la, lv, node;      /* node: the node they belong to, 0xFF: none */
+};
+DSM_HD void ser_cache_clear(SCache &c) { c.ct = c.la = c.lv = 0u; c.node = 0xFFu; }
+
 template <int NP, class M, class F>
-DSM_HD bool ser_macro(M &m, SReg &r, F &&fetch) {
+DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
     const uint32_t n = s_ctz(r.A), bit = 1u << n;
-    uint32_t ct = m.ld(S_CT + n);
+    const bool hot = cc.node == n;
+    uint32_t ct = hot ? cc.ct : m.ld(S_CT + n);
     const uint32_t ip = ct >> SC_IP;
     if (ip >= s_ni(r, n)) return false;                       /* the dump: one action */
-    const uint32_t ins = fetch(n, ip, true);
+    uint32_t ins;
+    if (!fetch(n, ip, ins)) return false;                     /* not at hand: ser_step loads it */
     const uint32_t a = (ins >> 8) & 0x7Fu, wr = ins >> 15, val = ins & 0xFFu;
     const uint32_t h = a >> 4, b = a & 15u, idx = a & 3u, sh8 = 8u * idx;
-    const uint32_t laW = m.ld(S_LA + n), lvW = m.ld(S_LV + n);
+    const uint32_t laW = hot ? cc.la : m.ld(S_LA + n), lvW = hot ? cc.lv : m.ld(S_LV + n);
     const uint32_t La = (laW >> sh8) & 0xFFu, Lv = (lvW >> sh8) & 0xFFu;
     const uint32_t lsh = SC_LS + 2u * idx, Ls = (ct >> lsh) & 3u;          /* M0 E1 S2 I3 */
     const bool hit = (La == a) & (Ls != 3u);                   /* :608, :635 */
@@ -414,12 +426,12 @@ DSM_HD bool ser_macro(M &m, SReg &r, F &&fetch) {
     const bool miss = !hit;
     const bool ev = miss & (La != 0xFFu) & (Ls != 3u);         /* :616-618, :670-672 */
     /* the victim's home vh, block vb; the request's home h, block b (every home < NP: a line
-     * holds an address some request brought in; h is checked) */
+     * holds an address some request brought in; h is checked).  All four words are read at
+     * once; the request's home sees the eviction's effect when they share a word. */
     const uint32_t vh = (La >> 4) & 7u, vb = La & 15u;
     const uint32_t wV = S_MB + 8u * vh + (vb >> 1), wH = S_MB + 8u * h + (b >> 1);
     const uint32_t mbV = m.ld(wV), dsV = m.ld(S_DS + vh);
-    uint32_t mbH = m.ld(wH), dsH = m.ld(S_DS + h);
-    bool ok = (NP == 8) || (h < (uint32_t)NP);
+    const uint32_t mbH0 = m.ld(wH), dsH0 = m.ld(S_DS + h);
     /* the eviction at the victim's home (:498-561); nothing is sent but the upgrade notice */
     const uint32_t hv = 16u * (vb & 1u), sv = 2u * vb;
     const uint32_t memV = (mbV >> hv) & 0xFFu, bvV = (mbV >> (hv + 8u)) & 0xFFu, dV = (dsV >> sv) & 3u;
@@ -427,70 +439,59 @@ DSM_HD bool ser_macro(M &m, SReg &r, F &&fetch) {
     const bool had = (bvV & bit) != 0u;
     const uint32_t bvS = bvV & ~bit;                            /* EVICT_SHARED, bit set */
     const uint32_t rem = (uint32_t)__builtin_popcount(bvS);
-    ok = ok & !(ev & !mod & had & (rem == 1u) & (dV == 1u));   /* S -> EM: notice (:507-519) */
-    uint32_t nbvV = bvV, ndV = dV, nmemV = memV;
-    if (mod) {                                                 /* EVICT_MODIFIED :544-547 */
-        nmemV = Lv;
-        const bool clr = (dV == 0u) & had;
-        nbvV = clr ? 0u : bvV;
-        ndV = clr ? 2u : dV;
-    } else if (had) {                                          /* EVICT_SHARED :501-508 */
-        nbvV = bvS;
-        ndV = rem == 0u ? 2u : dV;
-    }
+    const bool clrM = mod & (dV == 0u) & had;                   /* EVICT_MODIFIED :544-547 */
+    const uint32_t nmemV = mod ? Lv : memV;
+    const uint32_t nbvV = mod ? (clrM ? 0u : bvV) : (had ? bvS : bvV);        /* :501-508 */
+    const uint32_t ndV = mod ? (clrM ? 2u : dV) : ((had & (rem == 0u)) ? 2u : dV);
     const uint32_t mbV2 = (mbV & ~(0xFFFFu << hv)) | ((nmemV | (nbvV << 8)) << hv);
     const uint32_t dsV2 = (dsV & ~(3u << sv)) | (ndV << sv);
-    /* the request's home sees the eviction's effect when they share a word */
-    mbH = (ev & (wV == wH)) ? mbV2 : mbH;
-    dsH = (ev & (vh == h)) ? dsV2 : dsH;
+    const uint32_t mbH = (ev & (wV == wH)) ? mbV2 : mbH0;
+    const uint32_t dsH = (ev & (vh == h)) ? dsV2 : dsH0;
     const uint32_t hh = 16u * (b & 1u), shb = 2u * b;
     const uint32_t memH = (mbH >> hh) & 0xFFu, bvH = (mbH >> (hh + 8u)) & 0xFFu, dH = (dsH >> shb) & 3u;
     const uint32_t owner = s_ctz(bvH | 0x100u);                 /* findOwner :98-105 */
     const uint32_t others = bvH & ~bit;
-    /* EM at another owner: a forward (:222-232, :420-431); S with other sharers on a write or
-     * an upgrade: INV fan-out after REPLY_ID (:350-362); EM with no bit: the reference's
-     * assert (never reached, DESIGN) */
+    /* not applied here: the upgrade notice (S -> EM at the victim's home, :507-519); EM at
+     * another owner on a miss: a forward (:222-232, :420-431); S with other sharers on a write
+     * or an upgrade: INV fan-out after REPLY_ID (:350-362); EM with no bit: the reference's
+     * assert (never reached, DESIGN); a home >= NP: the defined ASSERT_FAILED */
+    const bool notice = ev & !mod & had & (rem == 1u) & (dV == 1u);
     const bool em_other = (dH == 0u) & (owner != n);
     const bool fan = (dH == 1u) & (others != 0u) & ((wr != 0u) | upg);
-    ok = ok & !(miss & em_other) & !((miss | upg) & fan);
+    const bool ok = ((NP == 8) || (h < (uint32_t)NP)) & !notice & !(miss & em_other) & !((miss | upg) & fan);
     if (!ok) return false;
-    /* the home's directory entry and memory after the request (:188-236, :298-328, :375-435) */
-    uint32_t nmemH = memH, nbvH = bvH, ndH = dH;
-    bool excl = true;                                          /* REPLY_RD's bitVector == 2 */
-    if (miss & (wr == 0u)) {                                    /* READ_REQUEST */
-        excl = dH != 1u;
-        nbvH = dH == 2u ? bit : (dH == 1u ? (bvH | bit) : bvH);
-        ndH = dH == 2u ? 0u : dH;
-    } else if (miss | upg) {                                    /* WRITE_REQUEST / UPGRADE */
-        nmemH = miss ? val : memH;
-        const bool keep = miss & (dH == 0u);                    /* EM at the requester */
-        nbvH = keep ? bvH : bit;
-        ndH = 0u;
-    }
-    if (miss | upg) {
-        m.st(S_DS + h, (dsH & ~(3u << shb)) | (ndH << shb));
-        m.st(wH, (mbH & ~(0xFFFFu << hh)) | ((nmemH | (nbvH << 8)) << hh));
-    }
-    if (ev) {   /* after the home's write when they share a word: that write holds both */
-        if (vh != h) m.st(S_DS + vh, dsV2);
-        if (wV != wH) m.st(wV, mbV2);
-    }
+    /* the home's directory entry and memory after the request (:188-236, :298-328, :375-435):
+     * READ_REQUEST U -> EM {n}, S -> S + n, EM at n unchanged; WRITE_REQUEST writes memory
+     * first, then U / S -> EM {n}, EM at n unchanged; UPGRADE -> EM {n} */
+    const bool rdq = miss & (wr == 0u), req = miss | upg;
+    const bool keep = (miss & (dH == 0u));                      /* EM at the requester */
+    const bool excl = !(rdq & (dH == 1u));                      /* REPLY_RD's bitVector == 2 */
+    const uint32_t nmemH = (miss & (wr != 0u)) ? val : memH;
+    const uint32_t nbvH = rdq ? (dH == 2u ? bit : (dH == 1u ? (bvH | bit) : bvH)) : (keep ? bvH : bit);
+    const uint32_t ndH = rdq ? (dH == 2u ? 0u : dH) : 0u;
+    /* write-back, branch-free (a disabled store goes to the dummy word); when the eviction's
+     * and the request's words coincide the request's write holds both */
+    m.st_if(req, S_DS + h, (dsH & ~(3u << shb)) | (ndH << shb));
+    m.st_if(req, wH, (mbH & ~(0xFFFFu << hh)) | ((nmemH | (nbvH << 8)) << hh));
+    m.st_if(ev & (vh != h), S_DS + vh, dsV2);
+    m.st_if(ev & (wV != wH), wV, mbV2);
     /* the requester's line (:243-246, :445-447, :334-336; a write hit :642-643, :656-657),
      * pendingWriteValue (:633), the instruction index */
     const uint32_t nLv = wr ? val : (miss ? memH : Lv);
     const uint32_t nLs = wr ? 0u : (miss ? (excl ? 1u : 2u) : Ls);
-    m.st(S_LA + n, (laW & ~(0xFFu << sh8)) | (a << sh8));
-    m.st(S_LV + n, (lvW & ~(0xFFu << sh8)) | (nLv << sh8));
+    const uint32_t nla = (laW & ~(0xFFu << sh8)) | (a << sh8);
+    const uint32_t nlv = (lvW & ~(0xFFu << sh8)) | (nLv << sh8);
     ct = (ct & ~(3u << lsh)) | (nLs << lsh);
-    ct = wr ? ((ct & ~0xFFu) | val) : ct;
-    m.st(S_CT + n, ct + (1u << SC_IP));
+    ct = (wr ? ((ct & ~0xFFu) | val) : ct) + (1u << SC_IP);
+    m.st(S_LA + n, nla);
+    m.st(S_LV + n, nlv);
+    m.st(S_CT + n, ct);
+    cc.ct = ct; cc.la = nla; cc.lv = nlv; cc.node = n;
     /* rounds: the issue, the handling round(s) -- two when the eviction and the request
      * queue at the same home -- and the reply; messages handled: eviction, request, reply */
     const bool lone = hit & !upg, twice = ev & (vh == h);
-    const uint32_t R = lone ? 1u : (twice ? 4u : 3u);
-    const uint32_t Mm = lone ? 0u : (ev ? 3u : 2u);
-    r.rounds += R;
-    r.msgs += Mm;
+    r.rounds += lone ? 1u : (twice ? 4u : 3u);
+    r.msgs += lone ? 0u : (ev ? 3u : 2u);
     r.E = 0u;
     return true;
 }

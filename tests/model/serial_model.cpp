@@ -90,17 +90,21 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         memset(dump, 0, sizeof dump);
         auto fetch = [&](uint32_t n, uint32_t i, bool iss) -> uint32_t { return iss ? tr[(size_t)n * stride + i] : 0u; };
         auto on_dump = [&](uint32_t n) { to_rec(m, n, 2u, &dump[n]); };
+        auto fetch_try = [&](uint32_t n, uint32_t i, uint32_t &ins) { ins = tr[(size_t)n * stride + i]; return true; };
         uint32_t v;
         bool sp = false;
+        dsms::SCache cc;
+        dsms::ser_cache_clear(cc);
         do {
             /* as the kernel: a lone node's whole transaction at once when it applies */
-            if (macro && cap >= 256u && dsms::ser_quiet_lone(r, lim) && dsms::ser_macro<NP>(m, r, fetch)) {
+            if (macro && cap >= 256u && dsms::ser_quiet_lone(r, lim) && dsms::ser_macro<NP>(m, r, cc, fetch_try)) {
                 ++n_macro;
                 v = dsms::SR_RUN;
                 continue;
             }
             v = cap < 256u ? dsms::ser_step<NP, Q, true>(m, r, T, fetch, on_dump, lim, cap)
                            : dsms::ser_step<NP, Q, false>(m, r, T, fetch, on_dump, lim, cap);
+            dsms::ser_cache_clear(cc);
             sp = sp || dsms::s_sq(r.q) != 0u;
         } while (v == dsms::SR_RUN);
         spilled += sp;

@@ -176,5 +176,5 @@ def test_one_pass_pair_reports_the_kernel_that_ran(dsm, orc, dist, picked):
         eng.run_packed(tr[:0], cn[:0])
         info = eng.launch_info()
         assert info["grid_blocks"] == 0 and info["ff_picked"] == 0 and info["resume_form"] == 0, info
-    ores, _ = orc.run_packed(8, tr, cn, nthreads=16)
+    ores = orc.run_packed(8, tr, cn, nthreads=16)[0]
     _cmp(res, ores)

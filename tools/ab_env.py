@@ -49,7 +49,9 @@ for r in range(reps):
         res[v].append(ms)
         if raw[:5].any():       # SER_PROBE builds: serial-pass event counts per wave
             print(f"{v}: probe iterations {int(raw[0])} macro {int(raw[1])} one-action {int(raw[2])} "
-                  f"chunk-miss {int(raw[3])} hand-over {int(raw[4])} wave_rounds {int(raw[26])}", flush=True)
+                  f"chunk-miss {int(raw[3])} hand-over {int(raw[4])} wave_rounds {int(raw[26])} "
+                  f"cycles macro {int(raw[5])} one-action {int(raw[6])} hand-over {int(raw[7])} "
+                  f"refill {int(raw[8])}", flush=True)
         info[v] = eng.launch_info()
 for v in variants:
     print(f"{var}={v} [{dist}, {n} systems]: kernel ms median {np.median(res[v]):.2f} "

@@ -6,5 +6,5 @@
 D=$1; N=$2; shift 2
 for L in "$@"; do
   if [ "$L" = default ]; then unset DSM_LIB; else export DSM_LIB=$L; fi
-  timeout -k 10 300 python tools/ab_env.py DSM_NONE 0 $N 3 $D 2>&1 | grep "kernel ms" | sed "s|^|$L: |" || exit 1
+  timeout -k 10 300 python tools/ab_env.py DSM_NONE 0 $N 3 $D 2>&1 | grep "kernel ms\|probe" | sed "s|^|$L: |" || exit 1
 done
