@@ -87,6 +87,13 @@ struct SimArgs {
     uint32_t *spill;                /* serial resume: [lane][S_SPILL] queue spill FIFOs      */
     uint32_t thr_ff;                /* budget pass, fast-forward kernel: suspend at this many
                                      * rounds (0: at 1 << rsh)                               */
+    uint32_t lone;                  /* budget pass with a serial resume: every `lone` rounds,
+                                     * suspend the systems that have become quiet-lone (one
+                                     * node may act, nothing queued) -- the serial pass's
+                                     * macro-step takes them (0: off)                        */
+    uint32_t lone_min;              /* ... once they have run at least this many rounds        */
+    uint32_t serfmt;                /* budget pass: suspended states in serial form (ssusp_words)
+                                     * unless the fast-forward pair's pick resumes them      */
 };
 /* the argument blocks of one run, written to device memory by args_kernel (stream-ordered:
  * no pinned staging whose reuse would need a host wait) */
@@ -118,6 +125,14 @@ static_assert((1u << RSH_MAX) == DSM_MAX_ROUNDS, "DSM_MAX_ROUNDS");
 /* suspended node state: memory/bitVector (8), lines (4), ring (RING), dst, ctl, ip, nins, rh,
  * nmsg, rounds (7), trace chunks cur, nxt (8) */
 constexpr int susp_words(int ring) { return 27 + ring; }
+/* the suspended state in serial form (a budget pass whose resume pass is ser_kernel): one
+ * contiguous record per system, so the resume reads it with 16-byte row loads --
+ *   [0, 96)    the serial pass's LDS column (dsm_serial.h S_MB .. S_CT), as it will be;
+ *   [96, 104)  per node: ring head | count << 8;  [104, 112) instructions in the trace;
+ *   [112, 120) messages received;  [120] rounds;
+ *   [128, 128 + 8 RING)  per node: its queued ring entries, oldest first (count of them). */
+constexpr int SSUSP_HDR = 128;
+constexpr int ssusp_words(int ring) { return SSUSP_HDR + 8 * ring; }
 
 constexpr uint64_t NO_SYS = ~0ull;
 constexpr uint32_t DSM_LINE_INIT = 0xFFu | (3u << 16);   /* address 0xFF, value 0, INVALID */
@@ -385,6 +400,9 @@ sim_kernel(const SimArgs *Ap) {
     /* hit-run fast-forward: wherever the order of issues inside a round is not observed
      * (not with the issue-order trace or the seeded stalls of schedule exploration) */
     constexpr bool FF = (MODE & (M_TR | M_SX | M_NOFF)) == 0;
+    /* suspend-on-lone and the serial-form record: the plain budget kernel only (with the
+     * fast-forward pair the plain one runs the budget pass of every serial-resumed run) */
+    constexpr bool LONE = BUD && !FF;
     constexpr int SW = susp_words(RING);
     /* fast-forward probe interval: FF_PROBE iterations after a probe that found a group,
      * doubling up to FF_PROBE_MAX after each one that found none (workloads without hit
@@ -434,6 +452,13 @@ sim_kernel(const SimArgs *Ap) {
         thr = Ap->thr_ff;          /* a fast-forward workload's budget (thr_ff, run_engine) */
     const uint32_t late_rsh = BUD ? Ap->late_rsh : 0u;
     const bool budget = BUD && Ap->budget != 0, resume = BUD && Ap->resume != 0;
+    /* suspend-on-lone: the budget pass of a run whose resume pass is the serial one (not the
+     * fast-forward pair's pick) */
+    const uint32_t lone_on = (LONE && budget && !(Ap->ffsel && ff_verdict(Ap->scan))) ? Ap->lone : 0u;
+    uint32_t lcd = lone_on;             /* rounds to the next check (uniform) */
+    uint64_t lonem = 0;                 /* lanes of the groups to suspend this round (uniform) */
+    const uint32_t lone_min = Ap->lone_min;   /* not before this many rounds */
+    const bool ser_fmt = LONE && budget && Ap->serfmt && !(Ap->ffsel && ff_verdict(Ap->scan));
     /* systems started statically (one per slot), the rest claimed from the shard counters.
      * The resume pass is launched at the full grid and sizes itself here from the device-
      * resident count of suspended systems (no host round trip): it uses the fewest slots
@@ -842,9 +867,10 @@ sim_kernel(const SimArgs *Ap) {
             uint32_t opv = op;
             asm volatile("" : "+v"(opv));
             const uint64_t actb = __ballot(opv != OP_IDLE || stall) | (WFF ? ffm : 0ull);
+            const uint64_t loneb = WFF ? 0ull : lonem;      /* (lone_mask, before the round) */
             /* rounds >= thr: the round limit, or the budget pass's budget */
             const uint64_t flagb = __ballot((nd.ctl & C_ASSERT) != 0u || rounds >= thr) |
-                                   __ballot(nccv > ocap);
+                                   __ballot(nccv > ocap) | loneb;
             constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
             constexpr uint64_t GHI = GLO << (NP - 1);
             const uint64_t t = actb | ~liveb;
@@ -855,7 +881,8 @@ sim_kernel(const SimArgs *Ap) {
             const bool gbad = ((badb >> gbase) & NPM) != 0;
             if (gact == 0) --rounds;
             /* budget pass: a system still running after thr rounds is suspended */
-            const bool susp = budget && gact != 0 && !gbad && rounds >= thr && (rounds >> lim_rsh) == 0u;
+            const bool lone = ((loneb >> lane) & 1ull) != 0ull;
+            const bool susp = budget && gact != 0 && !gbad && (rounds >= thr || lone) && (rounds >> lim_rsh) == 0u;
             const bool done = live && (gact == 0 || gbad || (rounds >> lim_rsh) != 0u || susp);
 
             const uint64_t doneb = __ballot(done);
@@ -874,7 +901,33 @@ sim_kernel(const SimArgs *Ap) {
                     const bool handoff = !FB && (st == DSM_RING_OVERFLOW);
                     const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
                     if (!handoff && !susp) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
-                    if (susp) {               /* save the node for the resume pass (start()) */
+                    if (susp && ser_fmt) {    /* the serial pass's record (ssusp_words) */
+                        uint32_t *sp = Ap->susp + sys * (uint64_t)ssusp_words(RING);
+                        uint4 *mb = reinterpret_cast<uint4 *>(sp + 8u * node);     /* S_MB + 8 n */
+                        mb[0] = make_uint4(s_mb[wv][0][lane], s_mb[wv][1][lane], s_mb[wv][2][lane], s_mb[wv][3][lane]);
+                        mb[1] = make_uint4(s_mb[wv][4][lane], s_mb[wv][5][lane], s_mb[wv][6][lane], s_mb[wv][7][lane]);
+                        uint32_t la = 0, lv = 0, ls = 0;
+    #pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t l = s_line[wv][i][lane];
+                            la |= (l & 0xFFu) << (8 * i);
+                            lv |= ((l >> 8) & 0xFFu) << (8 * i);
+                            ls |= ((l >> 16) & 3u) << (2 * i);
+                        }
+                        sp[64 + node] = la;                                 /* S_LA */
+                        sp[72 + node] = lv;                                 /* S_LV */
+                        sp[80 + node] = nd.dst;                             /* S_DS */
+                        sp[88 + node] = (nd.ctl & 0x3FFu) | (ls << 10) | (nd.ip << 18);   /* S_CT */
+                        sp[96 + node] = nd.rh;
+                        sp[104 + node] = nd.nins;
+                        sp[112 + node] = nd.nmsg;
+                        if (node == 0) sp[120] = rounds;
+                        const uint32_t h0 = nd.rh & 0xFFu, c0 = nd.rh >> 8;
+                        for (uint32_t j = 0; j < c0; ++j) {      /* queued messages, oldest first */
+                            const uint32_t sl = h0 + j;
+                            sp[SSUSP_HDR + node * RING + j] = s_ring[wv][sl >= (uint32_t)RING ? sl - RING : sl][lane];
+                        }
+                    } else if (susp) {        /* save the node for the resume pass (start()) */
                         uint32_t *sp = Ap->susp + sys * (uint64_t)(SW * NP) + node;
     #pragma unroll
                         for (int i = 0; i < 8; ++i) sp[i * NP] = s_mb[wv][i][lane];
@@ -947,6 +1000,7 @@ sim_kernel(const SimArgs *Ap) {
                     }
                 }
             }
+            lonem = 0;                     /* every lone group was suspended just now */
             const uint64_t nlive = __ballot(live);
             /* budget pass: once a slot of this wave found no new system, the wave's remaining
              * systems get the late budget, so the launch's tail is not a system claimed last
@@ -959,6 +1013,22 @@ sim_kernel(const SimArgs *Ap) {
      * one (no fast-forward code at all) and, while some group is in fast-forward mode, the
      * one with the fast-forward step (0).  Separate inner loops keep the plain loop's
      * register allocation and code as if fast-forward did not exist. */
+    /* budget pass with a serial resume, every `lone` rounds: the groups that are quiet and
+     * lone at the start of a round -- every inbox empty, exactly one node neither waiting nor
+     * dumped, with instructions left -- are suspended at the end of it (lonem); the serial
+     * pass applies such a node's whole transactions at once (dsm_serial.h ser_macro) where
+     * this kernel takes ~3 rounds of 8 lanes each.  Once lone, a system stays lone (the
+     * replies its waiting nodes wait for can no longer come). */
+    auto lone_mask = [&]() -> uint64_t {
+        const bool may = (nd.ctl & (C_WAIT | C_DUMPED)) == 0u;
+        const uint64_t qb = __ballot(nd.rh >= 256u);                        /* inbox non-empty */
+        const uint64_t ib = __ballot(may);                                  /* may act          */
+        const uint64_t pb = __ballot(may && nd.ip < nd.nins);                /* ... and issue    */
+        const uint32_t fq = (uint32_t)(qb >> gbase) & NPM, fi = (uint32_t)(ib >> gbase) & NPM;
+        const uint32_t fp = (uint32_t)(pb >> gbase) & NPM;
+        return __ballot(live && fq == 0u && fi != 0u && (fi & (fi - 1u)) == 0u && fp == fi &&
+                        rounds >= lone_min);
+    };
     uint32_t pint = FF_PROBE, pcd = FF_PROBE;   /* probe interval / countdown (uniform) */
     auto probe = [&]() {
         /* a group enters fast-forward mode when its inboxes are all empty, no node is about
@@ -1008,6 +1078,10 @@ sim_kernel(const SimArgs *Ap) {
             if (FF && --pcd == 0u) {
                 probe();
                 if (ffm) break;
+            }
+            if (LONE && lone_on && --lcd == 0u) {
+                lcd = lone_on;
+                lonem = lone_mask();
             }
             round(std::false_type{});
         }
@@ -1166,13 +1240,17 @@ ser_kernel(const SimArgs *Ap) {
         sys = list[n - 1 - k];             /* last-suspended first, as the lock-step resume */
         return true;
     };
-    /* the lock-step state the budget pass suspended (sim_kernel's layout [word][node]):
-     * memory / bitVector words as they are, cache lines (addr | value << 8 | state << 16)
-     * split into the address, value and control words, every inbox appended to the queue
-     * (node by node: only each inbox's own order matters) */
-    auto start = [&]() -> uint32_t {
+    /* the state the budget pass suspended, in serial form (ssusp_words): the LDS column as
+     * it is, in 16-byte row loads (two batches of 12, all in flight at once), then the
+     * per-node header -- ring position, trace length, messages received -- and each
+     * inbox's queued messages appended to the system's queue node by node (only each
+     * inbox's own order matters; a lone system has none) */
+    /* the same from the lock-step layout ([word][node], susp_words: a budget pass that ran
+     * in the fast-forward kernel of a run with limits, M_LIM): memory / bitVector words as
+     * they are, cache lines (addr | value << 8 | state << 16) split into the address, value
+     * and control words */
+    auto start_ls = [&]() {
         const GU32 *sp = (const GU32 *)(susp + sys * ((uint64_t)susp_words((int)SR) * NP));
-        ser_clear(r);
         r.rounds = sp[(12u + SR + 6u) * NP];
         for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {
             const GU32 *b = sp + nd;
@@ -1204,6 +1282,47 @@ ser_kernel(const SimArgs *Ap) {
             r.msgs += q[5 * NP] - c;       /* received - still queued = handled */
             r.iss |= ((ctl & (C_WAIT | C_DUMPED)) == 0u ? 1u : 0u) << nd;
             r.dmp |= ((ctl & C_DUMPED) ? 1u : 0u) << nd;
+        }
+    };
+    const bool serfmt = Ap->serfmt != 0u;   /* the format the budget pass wrote */
+    auto start = [&]() -> uint32_t {
+        ser_clear(r);
+        if (!serfmt) {
+            start_ls();
+        } else {
+        const GU32 *sp = (const GU32 *)(susp + sys * (uint64_t)ssusp_words((int)SR));
+        const GV4 *sv = (const GV4 *)sp;
+#pragma unroll
+        for (uint32_t bt = 0; bt < 2; ++bt) {
+            v4u32 x[12];
+#pragma unroll
+            for (uint32_t i = 0; i < 12; ++i) x[i] = sv[12u * bt + i];
+#pragma unroll
+            for (uint32_t i = 0; i < 12; ++i) {
+                const uint32_t w = 4u * (12u * bt + i);
+                m.st(w, x[i].x); m.st(w + 1u, x[i].y); m.st(w + 2u, x[i].z); m.st(w + 3u, x[i].w);
+            }
+        }
+        v4u32 hd[7];
+#pragma unroll
+        for (uint32_t i = 0; i < 7; ++i) hd[i] = sv[24u + i];
+        r.rounds = hd[6].x;
+        auto hw = [&](uint32_t k) -> uint32_t {        /* header word 96 + k, k < 24 (unrolled) */
+            const v4u32 &v = hd[k >> 2];
+            return (k & 3u) == 0u ? v.x : (k & 3u) == 1u ? v.y : (k & 3u) == 2u ? v.z : v.w;
+        };
+#pragma unroll
+        for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {
+            const uint32_t rh = hw(nd), c = rh >> 8, ctl = m.ld(S_CT + nd);
+            s_set_ni(r, nd, hw(8u + nd));
+            for (uint32_t j = 0; j < c; ++j)
+                ser_enqueue<S_QN>(m, r, nd, sp[SSUSP_HDR + nd * SR + j]);   /* <= 8 x 16: fits */
+            s_byte_add(r.cnt0, r.cnt1, nd, c);
+            r.nz |= (c ? 1u : 0u) << nd;
+            r.msgs += hw(16u + nd) - c;    /* received - still queued = handled */
+            r.iss |= ((ctl & (SC_WAIT | SC_DUMPED)) == 0u ? 1u : 0u) << nd;
+            r.dmp |= ((ctl & SC_DUMPED) ? 1u : 0u) << nd;
+        }
         }
         r.E = r.nz;
         r.A = r.nz | r.iss;
@@ -1627,7 +1746,7 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->ring = ring;
     c->cus = prop.multiProcessorCount;
     /* tuning knobs: read here once, reported by dsm_launch_info_get */
-    c->budget_log2 = env_u32("DSM_BUDGET_LOG2", 10);
+    c->budget_log2 = env_u32("DSM_BUDGET_LOG2", 12);
     if (c->budget_log2 >= RSH_MAX) c->budget_log2 = 0;
     /* the fast-forward kernel's budget in rounds (0: the plain budget); DSM_FF_BUDGET_LOG2,
      * if set, gives it as a power of two */
@@ -1641,6 +1760,9 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->inbox_limit = FB_RING;
     c->ff_mode = DSM_FF_AUTO;
     c->serial = (int)env_u32("DSM_SERIAL", 1);
+    /* the budget pass checks for quiet-lone systems every DSM_LONE rounds (0: never) */
+    c->lone_rounds = env_u32("DSM_LONE", 8);
+    c->lone_min = env_u32("DSM_LONE_MIN", 256);
     c->fmt_tile = (int)env_u32("DSM_FMT", 132);
     c->parse_bpl = (int)env_u32("DSM_PARSE_BPL", 32);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -1783,7 +1905,9 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     if ((rc = ensure(&c->d_ovf_list, &c->ovf_cap, (size_t)n_sys))) return rc;
     const int ring_eff = (mode && c->ring != 4) ? 12 : c->ring;   /* fast_mode's choice */
     if (blog) {
-        if ((rc = ensure(&c->d_susp, &c->susp_cap, (size_t)n_sys * np * susp_words(ring_eff)))) return rc;
+        const size_t sw = (size_t)np * susp_words(ring_eff) > (size_t)ssusp_words(ring_eff)
+                              ? (size_t)np * susp_words(ring_eff) : (size_t)ssusp_words(ring_eff);
+        if ((rc = ensure(&c->d_susp, &c->susp_cap, (size_t)n_sys * sw))) return rc;
         if ((rc = ensure(&c->d_susp_list, &c->susp_list_cap, (size_t)n_sys))) return rc;
     }
     if ((rc = ensure(&c->d_recs, &c->recs_cap, (size_t)n_sys * np * 8))) return rc;
@@ -1839,6 +1963,12 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
      * the fast-forward step and takes the plain budget. */
     A.budget = blog ? 1u : 0u;
     A.thr_ff = (mode == 0) ? c->ff_budget_rounds : 0u;
+    A.lone = (use_ser && (plain_only || pair)) ? c->lone_rounds : 0u;   /* serial resume only */
+    A.lone_min = c->lone_min;
+    /* the serial-form record and suspend-on-lone are compiled into the plain budget kernel
+     * only (sim_kernel LONE): runs whose budget pass takes it, the pair's plain half or the
+     * plain-only bench mode; with limits (M_LIM) the budget pass writes the lock-step form */
+    A.serfmt = (use_ser && (plain_only || pair)) ? 1u : 0u;
     A.late_rsh = (blog && c->late_log2 > 0 && c->late_log2 < blog) ? c->late_log2 : 0u;
     A.susp = c->d_susp;
     A.susp_list = c->d_susp_list;

@@ -58,6 +58,9 @@ struct dsm_ctx {
     uint32_t ff_budget_rounds;       /* ... as a round count, any value (DSM_FF_BUDGET_ROUNDS) */
     int ff_mode;                       /* DSM_FF_OFF / ON / AUTO */
     int serial;                        /* resume pass in serial form (ser_kernel; DSM_SERIAL) */
+    uint32_t lone_rounds;              /* budget pass: suspend quiet-lone systems, checked every
+                                        * this many rounds (DSM_LONE; 0: off)                  */
+    uint32_t lone_min;                 /* ... not before this many rounds (DSM_LONE_MIN)        */
     /* dsm_text.hip tuning (DSM_FMT / DSM_PARSE_BPL, read once at dsm_open) */
     int fmt_tile, parse_bpl;
     uint64_t sched_seed;             /* dsm_set_schedule                                     */

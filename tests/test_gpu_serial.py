@@ -171,3 +171,34 @@ def test_serial_small_ensembles(dsm, orc, monkeypatch, n):
     _cmp(res, ores)
     assert info["resume_form"] == 2 and info["resume_blocks"] == min(info["cus"], -(-n // 384)), info
     assert cnt["systems"] == n and cnt["resumed"] > 0
+
+
+@pytest.mark.parametrize("np_,dist,lone_min", [(8, "uniform", 0), (8, "evict", 0), (8, "uniform", 256),
+                                               (4, "uniform", 0)])
+def test_suspend_on_lone_is_exact(dsm, orc, monkeypatch, np_, dist, lone_min):
+    """The budget pass suspends quiet-lone systems (DSM_LONE, checked every 8 rounds, from
+    DSM_LONE_MIN rounds on) in the serial-form record; the serial pass resumes them with its
+    lone-node macro-step.  Results and records equal the oracle and a run without it, and the
+    suspensions are many more (every system that becomes lone early)."""
+    n = 4096
+    tr, cn = orc.generate(np_, dist, 13, 4096, 77, n)
+    ores, _, odump, ofin = orc.run_packed(np_, tr, cn, records=True, nthreads=16)
+    out = {}
+    for lone in ("0", "8"):
+        monkeypatch.setenv("DSM_LONE", lone)
+        monkeypatch.setenv("DSM_LONE_MIN", str(lone_min))
+        with dsm.Engine(np_, 4096, snapshots=True) as eng:
+            res, cnt = eng.run_packed(tr, cn)
+            assert eng.launch_info()["resume_form"] == 2
+            for s in range(0, n, 83):
+                mask = int(ores[s]["status"]) >> 8
+                for nd in range(np_):
+                    d, f = eng.node_state(s, nd)
+                    assert np.array_equal(f, ofin[s, nd])
+                    if (mask >> nd) & 1:
+                        assert np.array_equal(d, odump[s, nd])
+        _cmp(res, ores)
+        assert cnt["msgs"] == int(ores["msgs"].sum()) and cnt["overflow_reruns"] == 0
+        out[lone] = cnt
+    assert out["8"]["resumed"] > out["0"]["resumed"], (out["8"]["resumed"], out["0"]["resumed"])
+    assert out["8"]["sum_final_hash"] == out["0"]["sum_final_hash"]

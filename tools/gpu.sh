@@ -37,7 +37,7 @@ for s in "$@"; do
              step "kt_$a" 600 rocprofv3 --kernel-trace --stats --output-format csv \
                  -d "gpurun_out/prof_$a/kt" -o kt -- python3 bench.py --no-cpu --config "$b" \
                  --steps 3 --warmup 1 ;;
-    ab)      step "ab_${a}" 600 python -u tools/ab_open.py "$a" "$b" "${c:-1048576}" "${d:-2}" "${e:-uniform}" ;;
+    ab)      step "ab_${a}_${e:-uniform}" 600 python -u tools/ab_open.py "$a" "$b" "${c:-1048576}" "${d:-2}" "${e:-uniform}" ;;
     abl)     step "abl_${a}" 600 bash tools/ab_libs.sh "$a" "$b" ${c//,/ } ;;
     util)    step "util_$b" 300 env DSM_LIB="$a" python -u tools/lane_util.py "$b" ;;
     parse)   step text_tests 600 python -u -m pytest tests/test_gpu_text.py -x -q --timeout 240 --timeout-method thread
