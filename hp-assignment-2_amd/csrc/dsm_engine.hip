@@ -130,8 +130,12 @@ constexpr int susp_words(int ring) { return 27 + ring; }
  *   [0, 96)    the serial pass's LDS column (dsm_serial.h S_MB .. S_CT), as it will be;
  *   [96, 104)  per node: ring head | count << 8;  [104, 112) instructions in the trace;
  *   [112, 120) messages received;  [120] rounds;
- *   [128, 128 + 8 RING)  per node: its queued ring entries, oldest first (count of them). */
-constexpr int SSUSP_HDR = 128;
+ *   [121]      a lone system: its node | 0x100 (else 0), and [124, 128) / [128, 132) that
+ *              node's trace chunk ip >> 3 and the next (the lock-step shift register cur,
+ *              instructions ip.. in its low half-words, and nxt), so the serial pass's first
+ *              macro-step has its instruction at hand;
+ *   [136, 136 + 8 RING)  per node: its queued ring entries, oldest first (count of them). */
+constexpr int SSUSP_HDR = 136;
 constexpr int ssusp_words(int ring) { return SSUSP_HDR + 8 * ring; }
 
 constexpr uint64_t NO_SYS = ~0ull;
@@ -456,7 +460,6 @@ sim_kernel(const SimArgs *Ap) {
      * fast-forward pair's pick) */
     const uint32_t lone_on = (LONE && budget && !(Ap->ffsel && ff_verdict(Ap->scan))) ? Ap->lone : 0u;
     uint32_t lcd = lone_on;             /* rounds to the next check (uniform) */
-    uint64_t lonem = 0;                 /* lanes of the groups to suspend this round (uniform) */
     const uint32_t lone_min = Ap->lone_min;   /* not before this many rounds */
     const bool ser_fmt = LONE && budget && Ap->serfmt && !(Ap->ffsel && ff_verdict(Ap->scan));
     /* systems started statically (one per slot), the rest claimed from the shard counters.
@@ -611,6 +614,22 @@ sim_kernel(const SimArgs *Ap) {
             /* the pending value of the last write (a node that issued no write keeps its own) */
             nd.ctl = wm ? ((nd.ctl & ~0xFFu) | pv) : nd.ctl;     /* any write also set a line */
         }
+    };
+    /* budget pass with a serial resume, every `lone` rounds: the groups that are quiet and
+     * lone after a round's delivery -- every inbox empty, exactly one node neither waiting
+     * nor dumped, with instructions left -- are suspended at that round's end, before the
+     * lone node's next issue; the serial pass applies such a node's whole transactions at
+     * once (dsm_serial.h ser_macro) where this kernel takes ~3 rounds of 8 lanes each.  Once
+     * lone, a system stays lone (the replies its waiting nodes wait for can no longer come). */
+    auto lone_mask = [&]() -> uint64_t {
+        const bool may = (nd.ctl & (C_WAIT | C_DUMPED)) == 0u;
+        const uint64_t qb = __ballot(nd.rh >= 256u);                        /* inbox non-empty */
+        const uint64_t ib = __ballot(may);                                  /* may act          */
+        const uint64_t pb = __ballot(may && nd.ip < nd.nins);                /* ... and issue    */
+        const uint32_t fq = (uint32_t)(qb >> gbase) & NPM, fi = (uint32_t)(ib >> gbase) & NPM;
+        const uint32_t fp = (uint32_t)(pb >> gbase) & NPM;
+        return __ballot(live && fq == 0u && fi != 0u && (fi & (fi - 1u)) == 0u && fp == fi &&
+                        rounds >= lone_min);
     };
     /* one lock-step round of every system of the wave; compiled twice: with the
      * fast-forward step and its gating (WFF, while some group of the wave is in
@@ -867,7 +886,11 @@ sim_kernel(const SimArgs *Ap) {
             uint32_t opv = op;
             asm volatile("" : "+v"(opv));
             const uint64_t actb = __ballot(opv != OP_IDLE || stall) | (WFF ? ffm : 0ull);
-            const uint64_t loneb = WFF ? 0ull : lonem;      /* (lone_mask, before the round) */
+            uint64_t loneb = 0;
+            if (!WFF && LONE && lone_on && --lcd == 0u) {
+                lcd = lone_on;
+                loneb = lone_mask();
+            }
             /* rounds >= thr: the round limit, or the budget pass's budget */
             const uint64_t flagb = __ballot((nd.ctl & C_ASSERT) != 0u || rounds >= thr) |
                                    __ballot(nccv > ocap) | loneb;
@@ -922,6 +945,15 @@ sim_kernel(const SimArgs *Ap) {
                         sp[104 + node] = nd.nins;
                         sp[112 + node] = nd.nmsg;
                         if (node == 0) sp[120] = rounds;
+                        /* a lone system's node: its chunks (the group has one node that may act) */
+                        const bool mine = lone && (nd.ctl & (C_WAIT | C_DUMPED)) == 0u;
+                        if (mine) {
+                            reinterpret_cast<uint4 *>(sp + 124)[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
+                            reinterpret_cast<uint4 *>(sp + 128)[0] = make_uint4(nxt[0], nxt[1], nxt[2], nxt[3]);
+                            sp[121] = node | 0x100u;
+                        } else if (node == 0 && !lone) {
+                            sp[121] = 0u;
+                        }
                         const uint32_t h0 = nd.rh & 0xFFu, c0 = nd.rh >> 8;
                         for (uint32_t j = 0; j < c0; ++j) {      /* queued messages, oldest first */
                             const uint32_t sl = h0 + j;
@@ -1000,7 +1032,6 @@ sim_kernel(const SimArgs *Ap) {
                     }
                 }
             }
-            lonem = 0;                     /* every lone group was suspended just now */
             const uint64_t nlive = __ballot(live);
             /* budget pass: once a slot of this wave found no new system, the wave's remaining
              * systems get the late budget, so the launch's tail is not a system claimed last
@@ -1013,22 +1044,6 @@ sim_kernel(const SimArgs *Ap) {
      * one (no fast-forward code at all) and, while some group is in fast-forward mode, the
      * one with the fast-forward step (0).  Separate inner loops keep the plain loop's
      * register allocation and code as if fast-forward did not exist. */
-    /* budget pass with a serial resume, every `lone` rounds: the groups that are quiet and
-     * lone at the start of a round -- every inbox empty, exactly one node neither waiting nor
-     * dumped, with instructions left -- are suspended at the end of it (lonem); the serial
-     * pass applies such a node's whole transactions at once (dsm_serial.h ser_macro) where
-     * this kernel takes ~3 rounds of 8 lanes each.  Once lone, a system stays lone (the
-     * replies its waiting nodes wait for can no longer come). */
-    auto lone_mask = [&]() -> uint64_t {
-        const bool may = (nd.ctl & (C_WAIT | C_DUMPED)) == 0u;
-        const uint64_t qb = __ballot(nd.rh >= 256u);                        /* inbox non-empty */
-        const uint64_t ib = __ballot(may);                                  /* may act          */
-        const uint64_t pb = __ballot(may && nd.ip < nd.nins);                /* ... and issue    */
-        const uint32_t fq = (uint32_t)(qb >> gbase) & NPM, fi = (uint32_t)(ib >> gbase) & NPM;
-        const uint32_t fp = (uint32_t)(pb >> gbase) & NPM;
-        return __ballot(live && fq == 0u && fi != 0u && (fi & (fi - 1u)) == 0u && fp == fi &&
-                        rounds >= lone_min);
-    };
     uint32_t pint = FF_PROBE, pcd = FF_PROBE;   /* probe interval / countdown (uniform) */
     auto probe = [&]() {
         /* a group enters fast-forward mode when its inboxes are all empty, no node is about
@@ -1078,10 +1093,6 @@ sim_kernel(const SimArgs *Ap) {
             if (FF && --pcd == 0u) {
                 probe();
                 if (ffm) break;
-            }
-            if (LONE && lone_on && --lcd == 0u) {
-                lcd = lone_on;
-                lonem = lone_mask();
             }
             round(std::false_type{});
         }
@@ -1287,6 +1298,8 @@ ser_kernel(const SimArgs *Ap) {
     const bool serfmt = Ap->serfmt != 0u;   /* the format the budget pass wrote */
     auto start = [&]() -> uint32_t {
         ser_clear(r);
+        tn = 0xFFu;                         /* the fetch cache: empty */
+        nxv = pfv = false;
         if (!serfmt) {
             start_ls();
         } else {
@@ -1303,9 +1316,9 @@ ser_kernel(const SimArgs *Ap) {
                 m.st(w, x[i].x); m.st(w + 1u, x[i].y); m.st(w + 2u, x[i].z); m.st(w + 3u, x[i].w);
             }
         }
-        v4u32 hd[7];
+        v4u32 hd[9];
 #pragma unroll
-        for (uint32_t i = 0; i < 7; ++i) hd[i] = sv[24u + i];
+        for (uint32_t i = 0; i < 9; ++i) hd[i] = sv[24u + i];
         r.rounds = hd[6].x;
         auto hw = [&](uint32_t k) -> uint32_t {        /* header word 96 + k, k < 24 (unrolled) */
             const v4u32 &v = hd[k >> 2];
@@ -1323,12 +1336,33 @@ ser_kernel(const SimArgs *Ap) {
             r.iss |= ((ctl & (SC_WAIT | SC_DUMPED)) == 0u ? 1u : 0u) << nd;
             r.dmp |= ((ctl & SC_DUMPED) ? 1u : 0u) << nd;
         }
+        /* a lone system: its node's chunks into the fetch cache, the shift register re-aligned
+         * (instruction i of the chunk at half-word i; the consumed ones before ip read as 0) */
+        if (hd[6].y & 0x100u) {
+            tn = hd[6].y & 0xFFu;
+            const uint32_t ip0 = m.ld(S_CT + tn) >> SC_IP, j0 = ip0 & 7u;
+            const uint32_t rw[4] = {hd[7].x, hd[7].y, hd[7].z, hd[7].w};
+            uint32_t al[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (uint32_t k = 0; k < 8u; ++k) {        /* aligned half k = raw half k - j0 */
+                uint32_t hv = 0u;
+#pragma unroll
+                for (uint32_t q = 0; q < 8u; ++q)
+                    hv = (k >= j0 && k - j0 == q) ? ((rw[q >> 1] >> (16u * (q & 1u))) & 0xFFFFu) : hv;
+                al[k >> 1] |= hv << (16u * (k & 1u));
+            }
+            cur = make_uint4(al[0], al[1], al[2], al[3]);
+            nx = make_uint4(hd[8].x, hd[8].y, hd[8].z, hd[8].w);
+            tci = ip0 >> 3;
+            nxv = true;
+            pfc = tci + 2u;                /* and the chunk after, in flight */
+            pfv = pfc * 8u < stride;
+            if (pfv) pf = ld16(slot_of(tn) + pfc * 8u);
+        }
         }
         r.E = r.nz;
         r.A = r.nz | r.iss;
         ser_cache_clear(cc);
-        tn = 0xFFu;
-        nxv = pfv = false;
         if (r.A == 0u) {
             r.st = (r.dmp == NPM) ? SS_COMPLETED : SS_DEADLOCKED;
             return SR_DONE;
@@ -1359,9 +1393,12 @@ ser_kernel(const SimArgs *Ap) {
         tci = rot ? c : tci;
         if (__ballot(miss)) {            /* another node issues, or a system's first issue */
             if (SER_PROBE && lane == 0) atomicAdd(&s_cnt[3], 1ull);
-            if (miss) {
-                cur = ld16(slot_of(nd) + 8u * c);
-                pfv = nxv = false;
+            if (miss) {       /* the chunk and the next one, both waited for here */
+                const uint16_t *sl = slot_of(nd);
+                cur = ld16(sl + 8u * c);
+                nxv = (c + 1u) * 8u < stride;
+                nx = ld16(sl + (nxv ? 8u * (c + 1u) : 8u * c));
+                pfv = false;
                 tn = nd;
                 tci = c;
             }
@@ -1452,7 +1489,26 @@ ser_kernel(const SimArgs *Ap) {
                 for (int j = 0; j < SER_MACRO; ++j) {
                     const bool q = live && v == SR_RUN && ser_quiet_lone(r, lim_rsh) && (j == 0 || mac);
                     bool did = false;
+                    bool nohave = false;
+                    if (SER_PROBE && q) {         /* the instruction not at hand in registers */
+                        const uint32_t n0 = dsms::s_ctz(r.A), ip0 = m.ld(S_CT + n0) >> SC_IP, c0 = ip0 >> 3;
+                        nohave = !((tn == n0) & ((tci == c0) | ((tci + 1u == c0) & nxv)));
+                    }
                     if (__ballot(q) && q) did = ser_macro<NP>(m, r, cc, fetch_reg);
+                    if (SER_PROBE && j == 0) {
+                        const uint64_t nh = __ballot(nohave);
+                        if (lane == 0) atomicAdd(&s_cnt[8 + 3], 0ull + __builtin_popcountll(nh));
+                    }
+                    if (SER_PROBE && j == 0) {   /* lane-iterations left to ser_step, by cause */
+                        const bool nq_ = live && v == SR_RUN && !q;
+                        const uint64_t nq = __ballot(nq_), qn = __ballot(q && !did);
+                        const uint64_t mi = __ballot(nq_ && (r.iss & (r.iss - 1u)) != 0u);   /* several may act */
+                        if (lane == 0) {
+                            atomicAdd(&s_cnt[9], (unsigned long long)__builtin_popcountll(nq));
+                            atomicAdd(&s_cnt[10], (unsigned long long)__builtin_popcountll(qn));
+                            atomicAdd(&s_cnt[12], (unsigned long long)__builtin_popcountll(mi));
+                        }
+                    }
                     mac = mac || did;
                     nmac += did ? 1u : 0u;
                 }

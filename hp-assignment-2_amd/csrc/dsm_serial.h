@@ -394,9 +394,10 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
  * Not used in the CAP build (its per-node inbox counts are not kept here). */
 DSM_HD bool ser_quiet_lone(const SReg &r, uint32_t lim_rsh) {
     /* nothing queued or spilled, exactly one node may act and it is the only one left in the
-     * round, and the round limit is out of reach of the transaction's <= 4 rounds */
+     * round, and the round limit is out of reach of the transaction's <= 5 rounds and the
+     * round after (a fan-out's INVs) */
     return (r.nz | (r.q & 0xFFF8u) | r.spl) == 0u && r.A == r.iss && r.A != 0u && (r.A & (r.A - 1u)) == 0u &&
-           ((r.rounds + 4u) >> lim_rsh) == 0u;
+           ((r.rounds + 6u) >> lim_rsh) == 0u;
 }
 
 /* the lone node's own words (control, line addresses, line values) held in registers
@@ -427,22 +428,28 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
     const bool ev = miss & (La != 0xFFu) & (Ls != 3u);         /* :616-618, :670-672 */
     /* the victim's home vh, block vb; the request's home h, block b (every home < NP: a line
      * holds an address some request brought in; h is checked).  All four words are read at
-     * once; the request's home sees the eviction's effect when they share a word. */
+     * once; the request's home sees the eviction's effect when they share a word.  The
+     * victim's line has the same index as the request's (it is the line being replaced). */
     const uint32_t vh = (La >> 4) & 7u, vb = La & 15u;
     const uint32_t wV = S_MB + 8u * vh + (vb >> 1), wH = S_MB + 8u * h + (b >> 1);
     const uint32_t mbV = m.ld(wV), dsV = m.ld(S_DS + vh);
     const uint32_t mbH0 = m.ld(wH), dsH0 = m.ld(S_DS + h);
-    /* the eviction at the victim's home (:498-561); nothing is sent but the upgrade notice */
+    /* the eviction at the victim's home (:498-561) */
     const uint32_t hv = 16u * (vb & 1u), sv = 2u * vb;
     const uint32_t memV = (mbV >> hv) & 0xFFu, bvV = (mbV >> (hv + 8u)) & 0xFFu, dV = (dsV >> sv) & 3u;
     const bool mod = Ls == 0u;
     const bool had = (bvV & bit) != 0u;
     const uint32_t bvS = bvV & ~bit;                            /* EVICT_SHARED, bit set */
     const uint32_t rem = (uint32_t)__builtin_popcount(bvS);
+    /* EVICT_SHARED leaving one sharer x of an S entry: EM {x} and an upgrade notice to x
+     * (:507-519), handled by x in round 3 -- x's line, if it still holds the block in S,
+     * becomes EXCLUSIVE (:526-532) */
+    const bool notice = ev & !mod & had & (rem == 1u) & (dV == 1u);
+    const uint32_t x = s_ctz(bvS | 0x100u) & 7u;
     const bool clrM = mod & (dV == 0u) & had;                   /* EVICT_MODIFIED :544-547 */
     const uint32_t nmemV = mod ? Lv : memV;
     const uint32_t nbvV = mod ? (clrM ? 0u : bvV) : (had ? bvS : bvV);        /* :501-508 */
-    const uint32_t ndV = mod ? (clrM ? 2u : dV) : ((had & (rem == 0u)) ? 2u : dV);
+    const uint32_t ndV = mod ? (clrM ? 2u : dV) : (notice ? 0u : ((had & (rem == 0u)) ? 2u : dV));
     const uint32_t mbV2 = (mbV & ~(0xFFFFu << hv)) | ((nmemV | (nbvV << 8)) << hv);
     const uint32_t dsV2 = (dsV & ~(3u << sv)) | (ndV << sv);
     const uint32_t mbH = (ev & (wV == wH)) ? mbV2 : mbH0;
@@ -451,33 +458,64 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
     const uint32_t memH = (mbH >> hh) & 0xFFu, bvH = (mbH >> (hh + 8u)) & 0xFFu, dH = (dsH >> shb) & 3u;
     const uint32_t owner = s_ctz(bvH | 0x100u);                 /* findOwner :98-105 */
     const uint32_t others = bvH & ~bit;
-    /* not applied here: the upgrade notice (S -> EM at the victim's home, :507-519); EM at
-     * another owner on a miss: a forward (:222-232, :420-431); S with other sharers on a write
-     * or an upgrade: INV fan-out after REPLY_ID (:350-362); EM with no bit: the reference's
-     * assert (never reached, DESIGN); a home >= NP: the defined ASSERT_FAILED */
-    const bool notice = ev & !mod & had & (rem == 1u) & (dV == 1u);
-    const bool em_other = (dH == 0u) & (owner != n);
-    const bool fan = (dH == 1u) & (others != 0u) & ((wr != 0u) | upg);
-    const bool ok = ((NP == 8) || (h < (uint32_t)NP)) & !notice & !(miss & em_other) & !((miss | upg) & fan);
+    /* EM at another owner o on a miss: the home forwards WRITEBACK_INT / WRITEBACK_INV to o
+     * (:222-232, :420-431); o, holding the block in M or E, sends FLUSH / FLUSH_INVACK with its
+     * value to the home and the requester (:249-265, :451-467), which take it in the round
+     * after (:273-296, :475-496).  S with other sharers on a write or an upgrade: REPLY_ID
+     * names them and the requester sends each an INV (:350-362), taken in the round after
+     * (:366-373). */
+    const bool fwd = miss & (dH == 0u) & (owner != n);
+    const bool fan = (miss | upg) & (dH == 1u) & (others != 0u) & ((wr != 0u) | upg);
+    const uint32_t o = owner & 7u;
+    const uint32_t laO = m.ld(S_LA + o), lvO = m.ld(S_LV + o), ctO = m.ld(S_CT + o);
+    const bool oflush = (((laO >> sh8) & 0xFFu) == a) & (((ctO >> lsh) & 3u) <= 1u);
+    const uint32_t vO = (lvO >> sh8) & 0xFFu;                   /* the value o flushes */
+    /* not applied here (ser_step takes them one action at a time): a home >= NP (the defined
+     * ASSERT_FAILED), a forward to an owner without the block (the requester then waits for
+     * good), EM with no bit (the reference's assert; never reached, DESIGN), and the rare
+     * collisions whose inbox order would differ: the notice to the home or to the victim's
+     * home, or to the forward's owner, or to a sharer the fan-out also invalidates */
+    const bool ok = ((NP == 8) || (h < (uint32_t)NP)) & !(fwd & !oflush) &
+                    !((dH == 0u) & miss & (bvH == 0u)) &
+                    !(notice & ((x == h) | (x == vh) | (fwd & (x == o)) | (fan & (((others >> x) & 1u) != 0u))));
     if (!ok) return false;
     /* the home's directory entry and memory after the request (:188-236, :298-328, :375-435):
-     * READ_REQUEST U -> EM {n}, S -> S + n, EM at n unchanged; WRITE_REQUEST writes memory
-     * first, then U / S -> EM {n}, EM at n unchanged; UPGRADE -> EM {n} */
+     * READ_REQUEST U -> EM {n}, S -> S + n, EM at n unchanged, EM at o -> S {o, n};
+     * WRITE_REQUEST writes memory first, then U / S -> EM {n}, EM at n unchanged, EM at o ->
+     * EM {n}; UPGRADE -> EM {n}.  A flush then writes o's value to memory (FLUSH_INVACK also
+     * EM {n}: unchanged). */
     const bool rdq = miss & (wr == 0u), req = miss | upg;
-    const bool keep = (miss & (dH == 0u));                      /* EM at the requester */
-    const bool excl = !(rdq & (dH == 1u));                      /* REPLY_RD's bitVector == 2 */
-    const uint32_t nmemH = (miss & (wr != 0u)) ? val : memH;
-    const uint32_t nbvH = rdq ? (dH == 2u ? bit : (dH == 1u ? (bvH | bit) : bvH)) : (keep ? bvH : bit);
-    const uint32_t ndH = rdq ? (dH == 2u ? 0u : dH) : 0u;
+    const bool keep = miss & (dH == 0u) & !fwd;                 /* EM at the requester */
+    const bool excl = !(rdq & (dH == 1u)) & !fwd;               /* REPLY_RD's bitVector == 2 */
+    const uint32_t nmemH = fwd ? vO : ((miss & (wr != 0u)) ? val : memH);
+    const uint32_t nbvH = rdq ? (dH == 2u ? bit : ((dH == 1u) | fwd ? (bvH | bit) : bvH)) : (keep ? bvH : bit);
+    const uint32_t ndH = rdq ? (dH == 2u ? 0u : (fwd ? 1u : dH)) : 0u;
     /* write-back, branch-free (a disabled store goes to the dummy word); when the eviction's
      * and the request's words coincide the request's write holds both */
     m.st_if(req, S_DS + h, (dsH & ~(3u << shb)) | (ndH << shb));
     m.st_if(req, wH, (mbH & ~(0xFFFFu << hh)) | ((nmemH | (nbvH << 8)) << hh));
     m.st_if(ev & (vh != h), S_DS + vh, dsV2);
     m.st_if(ev & (wV != wH), wV, mbV2);
-    /* the requester's line (:243-246, :445-447, :334-336; a write hit :642-643, :656-657),
-     * pendingWriteValue (:633), the instruction index */
-    const uint32_t nLv = wr ? val : (miss ? memH : Lv);
+    /* the forward's owner: S after FLUSH, I after FLUSH_INVACK */
+    m.st_if(fwd, S_CT + o, (ctO & ~(3u << lsh)) | ((wr ? 3u : 2u) << lsh));
+    /* the notice's target: its line (same index) S -> E when it still holds the victim */
+    if (notice) {
+        const uint32_t laX = m.ld(S_LA + x), ctX = m.ld(S_CT + x);
+        const bool up = (((laX >> sh8) & 0xFFu) == La) & (((ctX >> lsh) & 3u) == 2u);
+        m.st_if(up, S_CT + x, (ctX & ~(3u << lsh)) | (1u << lsh));
+    }
+    /* the fan-out's sharers: a line holding the block in S or E becomes INVALID */
+    uint32_t fs = fan ? others : 0u;
+    while (fs) {
+        const uint32_t i = s_ctz(fs);
+        fs &= fs - 1u;
+        const uint32_t laI = m.ld(S_LA + i), ctI = m.ld(S_CT + i), lsI = (ctI >> lsh) & 3u;
+        const bool inv = (((laI >> sh8) & 0xFFu) == a) & ((lsI == 1u) | (lsI == 2u));
+        m.st_if(inv, S_CT + i, ctI | (3u << lsh));
+    }
+    /* the requester's line (:243-246, :291-294, :445-447, :334-336, :491-494; a write hit
+     * :642-643, :656-657), pendingWriteValue (:633), the instruction index */
+    const uint32_t nLv = fwd ? vO : (wr ? val : (miss ? memH : Lv));
     const uint32_t nLs = wr ? 0u : (miss ? (excl ? 1u : 2u) : Ls);
     const uint32_t nla = (laW & ~(0xFFu << sh8)) | (a << sh8);
     const uint32_t nlv = (lvW & ~(0xFFu << sh8)) | (nLv << sh8);
@@ -487,11 +525,18 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
     m.st(S_LV + n, nlv);
     m.st(S_CT + n, ct);
     cc.ct = ct; cc.la = nla; cc.lv = nlv; cc.node = n;
-    /* rounds: the issue, the handling round(s) -- two when the eviction and the request
-     * queue at the same home -- and the reply; messages handled: eviction, request, reply */
-    const bool lone = hit & !upg, twice = ev & (vh == h);
-    r.rounds += lone ? 1u : (twice ? 4u : 3u);
-    r.msgs += lone ? 0u : (ev ? 3u : 2u);
+    /* rounds: the issue; the request's round (2, or 3 when the eviction queued before it at
+     * the same home); a reply the round after -- or the forward's round, then the flush.
+     * The INVs after a REPLY_ID are taken in the round after the reply, the round of the
+     * node's next action: they touch only their receivers' lines, which that action does
+     * not read, so they are applied here and counted, and the round is the next one's.
+     * Messages handled: eviction, notice, request, reply or forward + one or two flushes,
+     * INVs. */
+    const bool lone = hit & !upg;
+    const uint32_t treq = (ev & (vh == h)) ? 3u : 2u;
+    r.rounds += lone ? 1u : treq + (fwd ? 2u : 1u);
+    r.msgs += lone ? 0u : (ev ? 1u : 0u) + (notice ? 1u : 0u) + 2u + (fwd ? (n != h ? 2u : 1u) : 0u) +
+                          (fan ? (uint32_t)__builtin_popcount(others) : 0u);
     r.E = 0u;
     return true;
 }

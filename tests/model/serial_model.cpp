@@ -80,7 +80,7 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
     const uint32_t lim = lim_log2 ? lim_log2 : 22;
     uint64_t compared = 0, ovf = 0, by_status[5] = {0, 0, 0, 0, 0};
     std::vector<uint32_t> col(dsms::S_WORDS), spill(dsms::S_SPILL);
-    uint64_t spilled = 0, n_macro = 0;
+    uint64_t spilled = 0, n_macro = 0, n_decl = 0, n_decl_dump = 0;
     for (uint64_t s = 0; s < n_sys; ++s) {
         HostCol m{col.data(), spill.data()};
         dsms::SReg r;
@@ -97,10 +97,15 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         dsms::ser_cache_clear(cc);
         do {
             /* as the kernel: a lone node's whole transaction at once when it applies */
-            if (macro && cap >= 256u && dsms::ser_quiet_lone(r, lim) && dsms::ser_macro<NP>(m, r, cc, fetch_try)) {
-                ++n_macro;
-                v = dsms::SR_RUN;
-                continue;
+            if (macro && cap >= 256u && dsms::ser_quiet_lone(r, lim)) {
+                if (dsms::ser_macro<NP>(m, r, cc, fetch_try)) {
+                    ++n_macro;
+                    v = dsms::SR_RUN;
+                    continue;
+                }
+                const uint32_t n0 = dsms::s_ctz(r.A);
+                if ((m.ld(dsms::S_CT + n0) >> dsms::SC_IP) >= dsms::s_ni(r, n0)) ++n_decl_dump;
+                else ++n_decl;
             }
             v = cap < 256u ? dsms::ser_step<NP, Q, true>(m, r, T, fetch, on_dump, lim, cap)
                            : dsms::ser_step<NP, Q, false>(m, r, T, fetch, on_dump, lim, cap);
@@ -142,9 +147,9 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         ++compared;
         ++by_status[r.st];
     }
-    printf("{\"systems\": %llu, \"compared\": %llu, \"ovf\": %llu, \"spilled\": %llu, \"macro\": %llu, \"by_status\": [%llu, %llu, %llu, %llu, %llu]}\n",
+    printf("{\"systems\": %llu, \"compared\": %llu, \"ovf\": %llu, \"spilled\": %llu, \"macro\": %llu, \"declined\": %llu, \"declined_dump\": %llu, \"by_status\": [%llu, %llu, %llu, %llu, %llu]}\n",
            (unsigned long long)n_sys, (unsigned long long)compared, (unsigned long long)ovf,
-           (unsigned long long)spilled, (unsigned long long)n_macro,
+           (unsigned long long)spilled, (unsigned long long)n_macro, (unsigned long long)n_decl, (unsigned long long)n_decl_dump,
            (unsigned long long)by_status[0], (unsigned long long)by_status[1],
            (unsigned long long)by_status[2], (unsigned long long)by_status[3],
            (unsigned long long)by_status[4]);
