@@ -1506,7 +1506,7 @@ ser_kernel(const SimArgs *Ap) {
                         if (lane == 0) {
                             atomicAdd(&s_cnt[9], (unsigned long long)__builtin_popcountll(nq));
                             atomicAdd(&s_cnt[10], (unsigned long long)__builtin_popcountll(qn));
-                            atomicAdd(&s_cnt[12], (unsigned long long)__builtin_popcountll(mi));
+                            (void)mi;
                         }
                     }
                     mac = mac || did;
@@ -1515,7 +1515,10 @@ ser_kernel(const SimArgs *Ap) {
             }
             if (SER_PROBE) {
                 const uint64_t gm = __ballot(live && v == SR_RUN && !mac), mm = __ballot(mac);
+                const uint64_t lv = __ballot(live);
                 if (lane == 0) {
+                    atomicAdd(&s_cnt[8], (unsigned long long)__builtin_popcountll(lv));   /* live lanes */
+                    if (__builtin_popcountll(lv) < 32) atomicAdd(&s_cnt[12], 1ull);
                     atomicAdd(&s_cnt[0], 1ull);
                     if (mm) atomicAdd(&s_cnt[1], 1ull);
                     if (gm) atomicAdd(&s_cnt[2], 1ull);
@@ -1546,7 +1549,7 @@ ser_kernel(const SimArgs *Ap) {
         uint64_t tr0 = 0;
         if (SER_PROBE >= 2) tr0 = __builtin_amdgcn_s_memtime();
         refill();
-        if (SER_PROBE >= 2 && lane == 0) atomicAdd(&s_cnt[8], __builtin_amdgcn_s_memtime() - tr0);
+        (void)tr0;
         iters += SER_RF;
         if (__ballot(live) == 0) break;
     }

@@ -467,9 +467,14 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
     const bool fwd = miss & (dH == 0u) & (owner != n);
     const bool fan = (miss | upg) & (dH == 1u) & (others != 0u) & ((wr != 0u) | upg);
     const uint32_t o = owner & 7u;
-    const uint32_t laO = m.ld(S_LA + o), lvO = m.ld(S_LV + o), ctO = m.ld(S_CT + o);
-    const bool oflush = (((laO >> sh8) & 0xFFu) == a) & (((ctO >> lsh) & 3u) <= 1u);
-    const uint32_t vO = (lvO >> sh8) & 0xFFu;                   /* the value o flushes */
+    bool oflush = false;
+    uint32_t ctO = 0u, vO = 0u;                                 /* o's control word, the value it flushes */
+    if (fwd) {            /* rare: the owner's line, read only then (a dependent LDS level) */
+        const uint32_t laO = m.ld(S_LA + o), lvO = m.ld(S_LV + o);
+        ctO = m.ld(S_CT + o);
+        oflush = (((laO >> sh8) & 0xFFu) == a) & (((ctO >> lsh) & 3u) <= 1u);
+        vO = (lvO >> sh8) & 0xFFu;
+    }
     /* not applied here (ser_step takes them one action at a time): a home >= NP (the defined
      * ASSERT_FAILED), a forward to an owner without the block (the requester then waits for
      * good), EM with no bit (the reference's assert; never reached, DESIGN), and the rare
