@@ -94,6 +94,8 @@ struct SimArgs {
     uint32_t lone_min;              /* ... once they have run at least this many rounds        */
     uint32_t serfmt;                /* budget pass: suspended states in serial form (ssusp_words)
                                      * unless the fast-forward pair's pick resumes them      */
+    uint32_t split;                 /* budget pass of the pair with a serial resume: the M_SERB
+                                     * plain kernel and the one without are both launched    */
 };
 /* the argument blocks of one run, written to device memory by args_kernel (stream-ordered:
  * no pinned staging whose reuse would need a host wait) */
@@ -334,7 +336,10 @@ enum : int {
     M_LIM = 8,  /* run-time round limit / inbox limit (dsm_set_round_limit,
                  * dsm_set_inbox_limit) for the bench mode, which otherwise has them as
                  * constants (measured: the two limits as SGPRs cost 1.5-2% in the round)  */
-    M_NOFF = 16 /* the bench mode without the hit-run fast-forward (ffscan_kernel picks)     */
+    M_NOFF = 16,/* the bench mode without the hit-run fast-forward (ffscan_kernel picks)     */
+    M_SERB = 32 /* with M_NOFF: the budget pass of a serial-resumed run (suspend-on-lone, the
+                 * serial-form record); the plain budget pass of a fast-forward-resumed run
+                 * is the kernel without them (measured on C4: 41.1 -> 40.0 ms per run)    */
 };
 
 /* ---- fast-forward verdict --------------------------------------------------------------
@@ -399,14 +404,14 @@ sim_kernel(const SimArgs *Ap) {
     constexpr uint32_t NPM = (1u << NP) - 1u;
     constexpr bool FB = (RING == FB_RING);   /* the 256-deep re-run kernel                */
     constexpr bool TC = (MODE & M_TC) != 0, TR = (MODE & M_TR) != 0, SX = (MODE & M_SX) != 0;
-    constexpr bool BUD = (MODE & ~(M_LIM | M_NOFF)) == 0 && !FB && !GEN;   /* two-pass schedule */
-    constexpr bool LIM = FB || (MODE & ~M_NOFF) != 0;   /* limits read at run time, else constants */
+    constexpr bool BUD = (MODE & ~(M_LIM | M_NOFF | M_SERB)) == 0 && !FB && !GEN;   /* two-pass schedule */
+    constexpr bool LIM = FB || (MODE & ~(M_NOFF | M_SERB)) != 0;   /* limits read at run time, else constants */
     /* hit-run fast-forward: wherever the order of issues inside a round is not observed
      * (not with the issue-order trace or the seeded stalls of schedule exploration) */
     constexpr bool FF = (MODE & (M_TR | M_SX | M_NOFF)) == 0;
-    /* suspend-on-lone and the serial-form record: the plain budget kernel only (with the
-     * fast-forward pair the plain one runs the budget pass of every serial-resumed run) */
-    constexpr bool LONE = BUD && !FF;
+    /* suspend-on-lone and the serial-form record: the plain budget kernel of a serial-resumed
+     * run only (M_SERB) */
+    constexpr bool LONE = BUD && !FF && (MODE & M_SERB) != 0;
     constexpr int SW = susp_words(RING);
     /* fast-forward probe interval: FF_PROBE iterations after a probe that found a group,
      * doubling up to FF_PROBE_MAX after each one that found none (workloads without hit
@@ -419,6 +424,9 @@ sim_kernel(const SimArgs *Ap) {
      * misses rather than hit runs, where the fast-forward step's probes only cost (C4: 48.2
      * -> 46.4 ms per step) */
     if (!FB && Ap->ffsel && (ff_verdict(Ap->scan) && !Ap->budget) != FF) return;
+    /* ... and of the two plain budget kernels (SimArgs::split), the one for the resume pass
+     * the verdict picked: M_SERB for the serial one, the other for the fast-forward one */
+    if (!FB && !FF && Ap->split && Ap->budget && ff_verdict(Ap->scan) == LONE) return;
 
     __shared__ uint32_t s_mb[WAVES][8][64];          /* 2 x (mem | bv << 8) per dword */
     __shared__ uint32_t s_line[WAVES][4][64];        /* cache lines: addr | value << 8 | state << 16 */
@@ -1681,8 +1689,8 @@ sim_fn fast_mode(int ring) {
      * the overflow-prone depth 4 (which exercises the 256-deep re-run) for the others */
     switch (ring) {
     case 4: return sim_kernel<NP, 4, FW, GEN, MODE>;
-    case 8: if ((MODE & ~M_NOFF) == 0) return sim_kernel<NP, 8, FW, GEN, MODE & M_NOFF>; break;
-    case 16: if ((MODE & ~M_NOFF) == 0) return sim_kernel<NP, 16, FW, GEN, MODE & M_NOFF>; break;
+    case 8: if ((MODE & ~(M_NOFF | M_SERB)) == 0) return sim_kernel<NP, 8, FW, GEN, MODE & (M_NOFF | M_SERB)>; break;
+    case 16: if ((MODE & ~(M_NOFF | M_SERB)) == 0) return sim_kernel<NP, 16, FW, GEN, MODE & (M_NOFF | M_SERB)>; break;
     default: break;
     }
     return sim_kernel<NP, 12, FW, GEN, MODE>;
@@ -1701,6 +1709,9 @@ sim_fn fast_np_gen(int ring, int mode) {
     case M_NOFF:                        /* packed path only (ffscan_kernel reads traces); the
                                          * fused generator has no plain kernel: mode 0 */
         if constexpr (!GEN) return fast_mode<NP, GEN, M_NOFF>(ring);
+        else return fast_mode<NP, GEN, 0>(ring);
+    case M_NOFF | M_SERB:
+        if constexpr (!GEN) return fast_mode<NP, GEN, M_NOFF | M_SERB>(ring);
         else return fast_mode<NP, GEN, 0>(ring);
     default: return fast_mode<NP, GEN, 0>(ring);
     }
@@ -1941,8 +1952,18 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
      * in auto, a pair of launches per pass, picked on the device by ffscan_kernel */
     const bool plain_only = mode == 0 && !gen && c->ff_mode == DSM_FF_OFF;
     const bool pair = mode == 0 && !gen && c->ff_mode == DSM_FF_AUTO;
-    const sim_fn fast = pick_fast(np, c->ring, gen, plain_only ? M_NOFF : mode), fb = pick_fallback(np, gen, mode);
+    /* two-pass schedule on the packed path in bench mode */
+    const uint32_t blog = ((mode & ~M_LIM) == 0 && !gen) ? c->budget_log2 : 0u;
+    /* the resume pass in serial form (ser_kernel) unless fast-forward is forced; with the
+     * fast-forward pair, the trace scan's verdict picks between it and the fast-forward
+     * lock-step resume */
+    const bool use_ser = blog && c->serial && c->ff_mode != DSM_FF_ON;
+    /* plain budget kernels: M_SERB (suspend-on-lone, serial-form record) where the serial
+     * pass resumes; the pair launches both and the verdict keeps one (SimArgs::split) */
+    const int plain_mode = use_ser ? (M_NOFF | M_SERB) : M_NOFF;
+    const sim_fn fast = pick_fast(np, c->ring, gen, plain_only ? plain_mode : mode), fb = pick_fallback(np, gen, mode);
     const sim_fn fast_nf = pair ? pick_fast(np, c->ring, gen, M_NOFF) : nullptr;
+    const sim_fn fast_serb = pair && use_ser ? pick_fast(np, c->ring, gen, M_NOFF | M_SERB) : nullptr;
     int nb_fast = 0, nb_fb = 0;
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fast, (const void *)fast, 64 * FW, 0));
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_fb, (const void *)fb, 64, 0));
@@ -1954,12 +1975,6 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     if (grid_fb > 1024) grid_fb = 1024;
     uint64_t dblocks = (n_sys * np + 255) / 256;
     if (dblocks > (uint64_t)c->cus * 8) dblocks = (uint64_t)c->cus * 8;
-    /* two-pass schedule on the packed path in bench mode */
-    const uint32_t blog = ((mode & ~M_LIM) == 0 && !gen) ? c->budget_log2 : 0u;
-    /* the resume pass in serial form (ser_kernel) unless fast-forward is forced; with the
-     * fast-forward pair, the trace scan's verdict picks between it and the fast-forward
-     * lock-step resume */
-    const bool use_ser = blog && c->serial && c->ff_mode != DSM_FF_ON;
     int rc;
     if ((rc = ensure(&c->d_ovf_list, &c->ovf_cap, (size_t)n_sys))) return rc;
     const int ring_eff = (mode && c->ring != 4) ? 12 : c->ring;   /* fast_mode's choice */
@@ -2028,6 +2043,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
      * only (sim_kernel LONE): runs whose budget pass takes it, the pair's plain half or the
      * plain-only bench mode; with limits (M_LIM) the budget pass writes the lock-step form */
     A.serfmt = (use_ser && (plain_only || pair)) ? 1u : 0u;
+    A.split = (pair && use_ser) ? 1u : 0u;
     A.late_rsh = (blog && c->late_log2 > 0 && c->late_log2 < blog) ? c->late_log2 : 0u;
     A.susp = c->d_susp;
     A.susp_list = c->d_susp_list;
@@ -2099,6 +2115,10 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
         } else if (pair) {
             hipLaunchKernelGGL(fast_nf, dim3(grid_fast), dim3(64 * FW), 0, st, a);
             HIPCK(hipGetLastError());
+            if (pass == 0 && fast_serb) {
+                hipLaunchKernelGGL(fast_serb, dim3(grid_fast), dim3(64 * FW), 0, st, a);
+                HIPCK(hipGetLastError());
+            }
         }
     }
     if (timed) {

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """tools/ab_open.py -- interleaved A/B of engine variants selected by an environment variable
-read at dsm_open (DSM_SERIAL, DSM_BUDGET_LOG2, DSM_LATE_LOG2, ...): a fresh engine per variant
+read at dsm_open (DSM_SERIAL, DSM_BUDGET_LOG2, DSM_LATE_LOG2, ...), or VAR=FF for the
+fast-forward mode (0 off, 1 on, 2 auto: dsm_set_fast_forward): a fresh engine per variant
 per repetition, traces generated once and resident in HBM; checks that every variant gives
 the same counters and hashes.
 
@@ -36,8 +37,11 @@ ctr = {}
 ref = None
 for r in range(reps):
     for v in variants:
-        os.environ[var] = v
+        if var != "FF":
+            os.environ[var] = v
         with pydsm.Engine(8, 4096, timing=True) as eng:
+            if var == "FF":
+                eng.set_fast_forward(int(v))
             cnt.zero_()
             eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
             torch.cuda.synchronize()
