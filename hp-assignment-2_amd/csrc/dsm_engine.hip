@@ -104,6 +104,16 @@ struct SimArgsPack { SimArgs a[3]; };
 
 #define DEVI __device__ __forceinline__
 
+#ifndef FF_LONG
+#define FF_LONG 1           /* fast-forward runs past the 8-instruction window */
+#endif
+#ifndef FF_LONG_U
+#define FF_LONG_U 8         /* trace chunks per step of that scan (hot, C4: 1 / 2 / 4 / 6 / 8 -> 49.6 / 39.3 / 34.1 / 32.6 / 32.1 ms) */
+#endif
+#ifndef FF_LONG_PIPE
+#define FF_LONG_PIPE 0      /* ... with the next step's chunks loaded during this one */
+#endif
+
 namespace {
 
 using namespace dsmg;
@@ -662,6 +672,7 @@ sim_kernel(const SimArgs *Ap) {
                 const bool inff = __builtin_amdgcn_inverse_ballot_w64(ffm);
                 if (lane == 0) s_cnt[wv][K_FFITER] += 1;     /* fast-forward steps of the wave */
                 uint32_t k = 8;
+                bool lng = false;          /* the group's step ran past the window (FF_LONG) */
                 if (inff) {
                     const bool iss = (nd.ctl & C_WAIT) == 0u && nd.ip < nd.nins;
                     const bool dpend = (nd.ctl & (C_WAIT | C_DUMPED)) == 0u && nd.ip >= nd.nins;
@@ -701,7 +712,76 @@ sim_kernel(const SimArgs *Ap) {
                     const uint32_t rmax = rounds + 1u >= thr ? 0u : thr - 1u - rounds;
                     if (r > rmax) r = rmax;
                     k = gmin<NP>(r);
-                    if (iss && k) {
+                    /* ---- the run past the window (FF_LONG) ---------------------------------
+                     * a group whose issuing nodes all hit the whole window scans on, FF_LONG_U
+                     * chunks per step straight from the trace, for the first miss of each node
+                     * (or its trace end, or the group's round bound rmax); k = the group's
+                     * minimum once every node has covered it.  The run applies at once, the
+                     * group leaves the mode and the round that breaks the run follows in this
+                     * iteration (C4 runs hundreds of hits per node between misses, where the
+                     * 8-wide window took one loop iteration per 8). */
+                    if (FF_LONG && __ballot(k == 8u)) {
+                        lng = k == 8u;                                    /* group-uniform */
+                        constexpr uint32_t INF = 0xFFFFFFFFu;
+                        const uint32_t nl = nd.nins - nd.ip;
+                        uint32_t found = iss ? (nl < rmax ? nl : rmax) : INF;
+                        uint32_t cc = (nd.ip >> 3) + 1u;     /* its first unscanned positions */
+                        bool go = lng;
+                        auto chunks = [&](uint32_t c, uint32_t (&w)[FF_LONG_U][4]) {
+    #pragma unroll
+                            for (int u = 0; u < FF_LONG_U; ++u) {
+                                if (GEN) {
+                                    gen_chunk<NP>(gmul, gdist, gfirst + sys, node, c + u, w[u]);
+                                } else {
+                                    const uint32_t pc = (c + u) * 8u;
+                                    const uint4 v = ld16(tb + (pc + 8u <= stride ? pc : stride - 8u));
+                                    w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
+                                }
+                            }
+                        };
+                        uint32_t wn[FF_LONG_U][4];       /* FF_LONG_PIPE: the next step's chunks */
+                        if (FF_LONG_PIPE && go && iss) chunks(cc, wn);
+                        while (__ballot(go)) {
+                            if (go) {
+                                if (iss) {
+                                    uint32_t w[FF_LONG_U][4];
+                                    if (FF_LONG_PIPE) {
+    #pragma unroll
+                                        for (int u = 0; u < FF_LONG_U; ++u)
+    #pragma unroll
+                                            for (int q = 0; q < 4; ++q) w[u][q] = wn[u][q];
+                                        chunks(cc + FF_LONG_U, wn);      /* in flight over this step */
+                                    } else {
+                                        chunks(cc, w);
+                                    }
+    #pragma unroll
+                                    for (int u = FF_LONG_U - 1; u >= 0; --u) {    /* the first miss wins */
+                                        const uint32_t xa = misses(w[u][0], w[u][1]), xb = misses(w[u][2], w[u][3]);
+                                        const uint32_t q = xa ? (uint32_t)__builtin_ctz(xa) >> 3
+                                                              : (xb ? 4u + ((uint32_t)__builtin_ctz(xb) >> 3) : 8u);
+                                        const uint32_t rel = 8u * (cc + u) + q - nd.ip;
+                                        found = (q < 8u && rel < found) ? rel : found;
+                                    }
+                                }
+                                /* every node's run is at least its coverage unless found */
+                                const uint32_t gc = gmin<NP>(iss ? 8u * (cc + FF_LONG_U) - nd.ip : INF);
+                                go = gmin<NP>(found) > gc;
+                                cc += FF_LONG_U;
+                            }
+                        }
+                        if (lng) k = gmin<NP>(found);
+                    }
+                    if (iss && k && lng) {
+                        if (!GEN) {     /* the shift register at the new position */
+                            const uint32_t ni = nd.ip + k, pc = (ni >> 3) * 8u;
+                            const uint4 v0 = ld16(tb + (pc + 8u <= stride ? pc : stride - 8u));
+                            const uint4 v1 = ld16(tb + (pc + 16u <= stride ? pc + 8u : stride - 8u));
+                            const uint32_t X[4] = {v0.x, v0.y, v0.z, v0.w};
+                            ff_shift(X, ni & 7u, cur);
+                            nxt[0] = v1.x; nxt[1] = v1.y; nxt[2] = v1.z; nxt[3] = v1.w;
+                        }
+                        nd.ip += k;
+                    } else if (iss && k) {
                         /* the write-back of the hits is deferred (ff_settle) */
                         if (!GEN) {     /* consume k from the shift register cur ++ nxt */
                             const bool cross = k >= m;
@@ -723,7 +803,7 @@ sim_kernel(const SimArgs *Ap) {
                 if (lane == 0) s_cnt[wv][K_FFPASS] += adv;   /* system steps that advanced */
                 /* those leave the mode and run this iteration's round normally, with their
                  * hits written back first */
-                const uint64_t leave = __ballot(inff && k < 8u);
+                const uint64_t leave = __ballot(inff && (k < 8u || lng));
                 ffm &= ~leave;
                 if (leave) ff_settle(__builtin_amdgcn_inverse_ballot_w64(leave));
             }
