@@ -1623,9 +1623,23 @@ ser_kernel(const SimArgs *Ap) {
                 if (lane == 0 && hm) atomicAdd(&s_cnt[4], 1ull);
             }
             if (live && v != SR_RUN) {
+                uint64_t th0 = 0, th1 = 0, th2 = 0;
+                if (SER_PROBE >= 3) th0 = __builtin_amdgcn_s_memtime();
                 finish(v);
+                if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th1 = __builtin_amdgcn_s_memtime(); }
                 live = claim();
+                if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th2 = __builtin_amdgcn_s_memtime(); }
                 v = live ? start() : SR_RUN;
+                if (SER_PROBE >= 3) {    /* hand-over cycles: finish, claim, start (lowest lane) */
+                    __builtin_amdgcn_s_waitcnt(0);
+                    const uint64_t th3 = __builtin_amdgcn_s_memtime();
+                    const uint64_t fl = __ballot(true);
+                    if (lane == (uint32_t)__builtin_ctzll(fl)) {
+                        atomicAdd(&s_cnt[13], th1 - th0);
+                        atomicAdd(&s_cnt[14], th2 - th1);
+                        atomicAdd(&s_cnt[15], th3 - th2);
+                    }
+                }
             }
             if (SER_PROBE >= 2 && lane == 0) {   /* cycles: macro phase, one-action phase, hand-over */
                 const uint64_t tp3 = __builtin_amdgcn_s_memtime();

@@ -26,17 +26,19 @@ import os
 import sys
 
 SIMDS, XCDS = 1024, 8
-KERNELS = {"sim_kernel_budget": "::sim_kernel<8, 12, 4, false, 16, 5>",
-           "sim_kernel_ff": "::sim_kernel<8, 12, 4, false, 0, 5>",
-           "ser_kernel": "::ser_kernel<8, false>"}
+# the plain budget kernel: M_NOFF (16) when the fast-forward kernel resumes, M_NOFF | M_SERB (48)
+# when the serial pass does
+KERNELS = {"sim_kernel_budget": ("::sim_kernel<8, 12, 4, false, 16, 5>", "::sim_kernel<8, 12, 4, false, 48, 5>"),
+           "sim_kernel_ff": ("::sim_kernel<8, 12, 4, false, 0, 5>",),
+           "ser_kernel": ("::ser_kernel<8, false>",)}
 
 
 def dispatches(path, pattern):
-    """{dispatch id: (wall ns, {counter: value})} of the kernels matching pattern."""
+    """{dispatch id: (wall ns, {counter: value})} of the kernels matching one of the patterns."""
     out = {}
     for f in glob.glob(os.path.join(path, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if pattern not in r["Kernel_Name"]:
+            if not any(p in r["Kernel_Name"] for p in pattern):
                 continue
             d = out.setdefault(r["Dispatch_Id"], [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
                                                   collections.defaultdict(float)])
