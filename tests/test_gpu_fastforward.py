@@ -2,7 +2,7 @@
 
 After a round in which a system sent nothing, every further round until some node issues a
 sending instruction is one local hit per non-waiting node (assignment.c:607-611 RD hit,
-:635-645 WR hit on M/E); the kernel applies such runs 8 rounds per step.  It must be exact:
+:635-645 WR hit on M/E); the kernel applies a whole such run per step (FF_LONG).  It must be exact:
 results (rounds included), records and counters equal the oracle's, and equal the kernel's
 own round-by-round path (the issue-order mode, which has no fast-forward)."""
 import os
@@ -178,3 +178,35 @@ def test_one_pass_pair_reports_the_kernel_that_ran(dsm, orc, dist, picked):
         assert info["grid_blocks"] == 0 and info["ff_picked"] == 0 and info["resume_form"] == 0, info
     ores = orc.run_packed(8, tr, cn, nthreads=16)[0]
     _cmp(res, ores)
+
+
+@pytest.mark.parametrize("ffb", [7, 100, 384, 1000])
+def test_long_runs_end_at_ragged_trace_ends_and_budgets(dsm, orc, monkeypatch, ffb):
+    """FF_LONG (dsm_engine.hip, the run past the 8-instruction window, 8 chunks per scan step)
+    must stop exactly at the group's first miss, at a trace end that is not a chunk boundary
+    (ragged counts) and at the budget (FF_ON: the fast-forward kernel runs the budget pass,
+    thr_ff = DSM_FF_BUDGET_ROUNDS rounds, so runs are cut mid-scan): against the oracle."""
+    n = 2048
+    tr, cn = orc.generate(8, "hot", 33, 4096, 900, n)
+    rng = np.random.default_rng(ffb)
+    cn = np.minimum(cn, rng.integers(1, 4097, size=cn.shape).astype(np.uint32))
+    ores = orc.run_packed(8, tr, cn, nthreads=16)[0]
+    monkeypatch.setenv("DSM_FF_BUDGET_ROUNDS", str(ffb))
+    with dsm.Engine(8, 4096) as eng:
+        for m in (dsm.FF_ON, dsm.FF_AUTO):
+            eng.set_fast_forward(m)
+            res, cnt = eng.run_packed(tr, cn)
+            _cmp(res, ores)
+            assert cnt["ff_steps"] > 0 and cnt["ff_passes"] > 0
+
+
+@pytest.mark.parametrize("n_instr", [1001, 2045])
+def test_long_runs_generated_path(dsm, orc, n_instr):
+    """The fused-generator kernel's long runs (chunks generated, not loaded) with a trace
+    length that ends inside a chunk."""
+    n = 2048
+    gres, _ = orc.run_generated(8, "hot", 41, n_instr, 300, n, nthreads=16)
+    with dsm.Engine(8, 4096) as eng:
+        res, cnt = eng.run_generated("hot", 41, n_instr, 300, n)
+    _cmp(res, gres)
+    assert cnt["ff_passes"] > 0
