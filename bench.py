@@ -573,7 +573,8 @@ def main():
             roof["issue_how"] = ("valu_busy = SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); "
                                  "waves_per_simd = SQ_WAVE_CYCLES x 4 / (GRBM_GUI_ACTIVE / 8) / 1024; "
                                  "wait_frac / issue_stall_frac = SQ_WAIT_ANY / SQ_WAIT_INST_ANY over "
-                                 "their sum with SQ_ACTIVE_INST_ANY; clock = GRBM_GUI_ACTIVE / 8 / wall")
+                                 "their sum with SQ_ACTIVE_INST_ANY; wait_per_wave_cycle = SQ_WAIT_ANY / "
+                                 "SQ_WAVE_CYCLES; clock = GRBM_GUI_ACTIVE / 8 / wall")
         for phase, kname in ((trace_parse, "parse_kernel"), (dump_stream, "fmt_kernel"),
                              (trace_stream, "gen_kernel")):
             if phase is not None and tr.get(kname):

@@ -15,6 +15,7 @@ Start/End timestamps):
 and from the pmc_wait pass (SQ_WAIT_ANY + SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY ~ the
 wave-cycles):
   wait_frac        = SQ_WAIT_ANY / that sum        (waves parked on a counter: s_waitcnt)
+  wait_per_wave_cycle = SQ_WAIT_ANY / SQ_WAVE_CYCLES (the SQ pass's per-dispatch mean)
   issue_stall_frac = SQ_WAIT_INST_ANY / that sum   (waves ready but not issued)
   lds_conflict_per_lds_inst = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS
 Averages over the dispatches; the per-launch instruction counts ride along."""
@@ -55,18 +56,23 @@ def summarize(d, pattern):
         cyc = c["GRBM_GUI_ACTIVE"] / XCDS
         rows.append(dict(ms=wall / 1e6, clock_ghz=cyc / wall, valu_busy=c["SQ_INSTS_VALU"] * 2 / (cyc * SIMDS),
                          waves_per_simd=c["SQ_WAVE_CYCLES"] * 4 / cyc / SIMDS, waves=c["SQ_WAVES"],
-                         valu=c["SQ_INSTS_VALU"], salu=c["SQ_INSTS_SALU"], lds=c["SQ_INSTS_LDS"]))
+                         valu=c["SQ_INSTS_VALU"], salu=c["SQ_INSTS_SALU"], lds=c["SQ_INSTS_LDS"],
+                         wave_cycles=c["SQ_WAVE_CYCLES"]))
     wrows = []
+    wave_cycles = sum(r["wave_cycles"] for r in rows) / len(rows)
     for _, c in wt.values():
         tot = c["SQ_WAIT_ANY"] + c["SQ_WAIT_INST_ANY"] + c["SQ_ACTIVE_INST_ANY"]
         wrows.append(dict(wait_frac=c["SQ_WAIT_ANY"] / tot, issue_stall_frac=c["SQ_WAIT_INST_ANY"] / tot,
+                          # the verdict's form: SQ_WAIT_ANY / SQ_WAVE_CYCLES (both quad-cycles; the
+                          # two counters come from separate passes: the SQ pass's per-dispatch mean)
+                          wait_per_wave_cycle=c["SQ_WAIT_ANY"] / max(wave_cycles, 1.0),
                           lds_bank_conflict_cycles=c["SQ_LDS_BANK_CONFLICT"],
                           lds_conflict_per_lds_inst=c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_ACTIVE_INST_LDS"], 1.0)))
     avg = lambda rs, k: sum(r[k] for r in rs) / len(rs)
     out = {k: avg(rows, k) for k in rows[0]}
     if wrows:
         out.update({k: avg(wrows, k) for k in wrows[0]})
-    rnd = {"ms": 3, "clock_ghz": 3, "valu_busy": 4, "waves_per_simd": 3, "wait_frac": 4,
+    rnd = {"ms": 3, "clock_ghz": 3, "valu_busy": 4, "waves_per_simd": 3, "wait_frac": 4, "wait_per_wave_cycle": 4,
            "issue_stall_frac": 4, "lds_conflict_per_lds_inst": 4}
     out = {k: (round(v, rnd[k]) if k in rnd else int(v)) for k, v in out.items()}
     out["dispatches"] = len(rows)
