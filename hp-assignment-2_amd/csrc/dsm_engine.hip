@@ -1245,6 +1245,12 @@ constexpr int SER_MACRO = SER_MACRO_DEF;   /* lone-node macro-steps per iteratio
 /* SER_PROBE builds (diagnostics, never the default): per-wave event counts of the serial pass
  * in the counter slots the pass leaves unused (msgs_by_type 0-4): iterations, iterations with
  * a macro-step, with a one-action step, with a chunk miss, hand-overs */
+#ifndef SER_HDR_FIRST
+#define SER_HDR_FIRST 1
+#endif
+#ifndef SER_CLAIM_EARLY
+#define SER_CLAIM_EARLY 1
+#endif
 #ifndef SER_PROBE
 #define SER_PROBE 0
 #endif
@@ -1393,6 +1399,12 @@ ser_kernel(const SimArgs *Ap) {
         } else {
         const GU32 *sp = (const GU32 *)(susp + sys * (uint64_t)ssusp_words((int)SR));
         const GV4 *sv = (const GV4 *)sp;
+        /* the header rows in flight with the first batch of the column's (SER_HDR_FIRST) */
+        v4u32 hd[9];
+        if (SER_HDR_FIRST) {
+#pragma unroll
+            for (uint32_t i = 0; i < 9; ++i) hd[i] = sv[24u + i];
+        }
 #pragma unroll
         for (uint32_t bt = 0; bt < 2; ++bt) {
             v4u32 x[12];
@@ -1404,9 +1416,10 @@ ser_kernel(const SimArgs *Ap) {
                 m.st(w, x[i].x); m.st(w + 1u, x[i].y); m.st(w + 2u, x[i].z); m.st(w + 3u, x[i].w);
             }
         }
-        v4u32 hd[9];
+        if (!SER_HDR_FIRST) {
 #pragma unroll
-        for (uint32_t i = 0; i < 9; ++i) hd[i] = sv[24u + i];
+            for (uint32_t i = 0; i < 9; ++i) hd[i] = sv[24u + i];
+        }
         r.rounds = hd[6].x;
         auto hw = [&](uint32_t k) -> uint32_t {        /* header word 96 + k, k < 24 (unrolled) */
             const v4u32 &v = hd[k >> 2];
@@ -1582,7 +1595,7 @@ ser_kernel(const SimArgs *Ap) {
                         const uint32_t n0 = dsms::s_ctz(r.A), ip0 = m.ld(S_CT + n0) >> SC_IP, c0 = ip0 >> 3;
                         nohave = !((tn == n0) & ((tci == c0) | ((tci + 1u == c0) & nxv)));
                     }
-                    if (__ballot(q) && q) did = ser_macro<NP>(m, r, cc, fetch_reg);
+                    if (__ballot(q) && q) did = ser_macro<NP>(m, r, cc, fetch_reg, on_dump);
                     if (SER_PROBE && j == 0) {
                         const uint64_t nh = __ballot(nohave);
                         if (lane == 0) atomicAdd(&s_cnt[8 + 3], 0ull + __builtin_popcountll(nh));
@@ -1600,6 +1613,8 @@ ser_kernel(const SimArgs *Ap) {
                     mac = mac || did;
                     nmac += did ? 1u : 0u;
                 }
+                /* a macro-step that ended the system (the dead-end forward): quiescent */
+                if (mac && r.A == 0u) v = SR_DONE;
             }
             if (SER_PROBE) {
                 const uint64_t gm = __ballot(live && v == SR_RUN && !mac), mm = __ballot(mac);
@@ -1625,9 +1640,18 @@ ser_kernel(const SimArgs *Ap) {
             if (live && v != SR_RUN) {
                 uint64_t th0 = 0, th1 = 0, th2 = 0;
                 if (SER_PROBE >= 3) th0 = __builtin_amdgcn_s_memtime();
+                /* SER_CLAIM_EARLY: the claim's atomic is issued before the finished system's
+                 * records are written, so its round trip overlaps them */
+                uint32_t k = 0;
+                if (SER_CLAIM_EARLY && SER_PROBE < 3) k = atomicAdd(claim_ctr, 1u);
                 finish(v);
                 if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th1 = __builtin_amdgcn_s_memtime(); }
-                live = claim();
+                if (SER_CLAIM_EARLY && SER_PROBE < 3) {
+                    live = k < n;
+                    if (live) sys = list[n - 1 - k];
+                } else {
+                    live = claim();
+                }
                 if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th2 = __builtin_amdgcn_s_memtime(); }
                 v = live ? start() : SR_RUN;
                 if (SER_PROBE >= 3) {    /* hand-over cycles: finish, claim, start (lowest lane) */

@@ -50,6 +50,16 @@
 #ifndef DSM_SERIAL_H
 #define DSM_SERIAL_H
 
+#ifndef SER_NOTICE_HOME
+#define SER_NOTICE_HOME 1   /* ... and an upgrade notice to either home */
+#endif
+#ifndef SER_DUMP
+#define SER_DUMP 0          /* ... and the lone node's dump (exact, but C5 33.4 vs 32.5 ms: off) */
+#endif
+#ifndef SER_DEAD_FWD
+#define SER_DEAD_FWD 1      /* ser_macro also applies a system's dead-end forward */
+#endif
+
 #include "dsm_table.h"
 
 namespace dsms {
@@ -408,13 +418,29 @@ struct SCache {
 };
 DSM_HD void ser_cache_clear(SCache &c) { c.ct = c.la = c.lv = 0u; c.node = 0xFFu; }
 
-template <int NP, class M, class F>
-DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
+template <int NP, class M, class F, class R>
+DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump) {
+    constexpr uint32_t NPM = (1u << NP) - 1u;
     const uint32_t n = s_ctz(r.A), bit = 1u << n;
     const bool hot = cc.node == n;
     uint32_t ct = hot ? cc.ct : m.ld(S_CT + n);
     const uint32_t ip = ct >> SC_IP;
-    if (ip >= s_ni(r, n)) return false;                       /* the dump: one action */
+    if (ip >= s_ni(r, n)) {
+        /* the trace is done: the dump (:688-697), the round's one action; then no node can
+         * act and the system is quiescent (the caller ends it when r.A is empty) */
+        if (!SER_DUMP) return false;
+        ct |= SC_DUMPED;
+        m.st(S_CT + n, ct);
+        r.dmp |= bit;
+        on_dump(n);                          /* printProcessorState(threadId, node), :695 */
+        r.iss &= ~bit;
+        r.A = r.iss;
+        r.rounds += 1u;
+        r.E = 0u;
+        r.st = (r.dmp == NPM) ? SS_COMPLETED : SS_DEADLOCKED;
+        cc.ct = ct; cc.node = n;
+        return true;
+    }
     uint32_t ins;
     if (!fetch(n, ip, ins)) return false;                     /* not at hand: ser_step loads it */
     const uint32_t a = (ins >> 8) & 0x7Fu, wr = ins >> 15, val = ins & 0xFFu;
@@ -446,10 +472,14 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
      * becomes EXCLUSIVE (:526-532) */
     const bool notice = ev & !mod & had & (rem == 1u) & (dV == 1u);
     const uint32_t x = s_ctz(bvS | 0x100u) & 7u;
+    /* ... and when x is the victim's home itself, it takes the notice (an EVICT_SHARED at the
+     * block's home, :498-505) as an eviction from itself: its bit cleared, none left, the entry
+     * UNOWNED, its own line untouched */
+    const bool selfn = SER_NOTICE_HOME & notice & (x == vh);
     const bool clrM = mod & (dV == 0u) & had;                   /* EVICT_MODIFIED :544-547 */
     const uint32_t nmemV = mod ? Lv : memV;
-    const uint32_t nbvV = mod ? (clrM ? 0u : bvV) : (had ? bvS : bvV);        /* :501-508 */
-    const uint32_t ndV = mod ? (clrM ? 2u : dV) : (notice ? 0u : ((had & (rem == 0u)) ? 2u : dV));
+    const uint32_t nbvV = mod ? (clrM ? 0u : bvV) : (selfn ? 0u : (had ? bvS : bvV));   /* :501-508 */
+    const uint32_t ndV = mod ? (clrM ? 2u : dV) : (notice ? (selfn ? 2u : 0u) : ((had & (rem == 0u)) ? 2u : dV));
     const uint32_t mbV2 = (mbV & ~(0xFFFFu << hv)) | ((nmemV | (nbvV << 8)) << hv);
     const uint32_t dsV2 = (dsV & ~(3u << sv)) | (ndV << sv);
     const uint32_t mbH = (ev & (wV == wH)) ? mbV2 : mbH0;
@@ -475,14 +505,20 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
         oflush = (((laO >> sh8) & 0xFFu) == a) & (((ctO >> lsh) & 3u) <= 1u);
         vO = (lvO >> sh8) & 0xFFu;
     }
+    /* a forward to an owner that no longer holds the block in M or E: the owner ignores it
+     * (:266-270, :468-472), no flush comes and the requester waits for good -- the system's
+     * last transaction (every other node waits or has dumped), applied here too: the home's
+     * directory and memory as for any forward, the requester's line as the miss left it
+     * (INVALID, the address, value 0, :623-625, :675-677), and the system ends */
+    const bool dead = fwd & !oflush;
     /* not applied here (ser_step takes them one action at a time): a home >= NP (the defined
-     * ASSERT_FAILED), a forward to an owner without the block (the requester then waits for
-     * good), EM with no bit (the reference's assert; never reached, DESIGN), and the rare
-     * collisions whose inbox order would differ: the notice to the home or to the victim's
-     * home, or to the forward's owner, or to a sharer the fan-out also invalidates */
-    const bool ok = ((NP == 8) || (h < (uint32_t)NP)) & !(fwd & !oflush) &
+     * ASSERT_FAILED), EM with no bit (the reference's assert; never reached, DESIGN), and the
+     * rare collisions whose inbox order would differ: the notice to the home or to the
+     * victim's home, or to the forward's owner, or to a sharer the fan-out also invalidates */
+    const bool ok = ((NP == 8) || (h < (uint32_t)NP)) & (SER_DEAD_FWD | !dead) &
                     !((dH == 0u) & miss & (bvH == 0u)) &
-                    !(notice & ((x == h) | (x == vh) | (fwd & (x == o)) | (fan & (((others >> x) & 1u) != 0u))));
+                    !(notice & ((((x == h) | (x == vh)) & !SER_NOTICE_HOME) | (fwd & (x == o)) |
+                                (fan & (((others >> x) & 1u) != 0u))));
     if (!ok) return false;
     /* the home's directory entry and memory after the request (:188-236, :298-328, :375-435):
      * READ_REQUEST U -> EM {n}, S -> S + n, EM at n unchanged, EM at o -> S {o, n};
@@ -492,7 +528,7 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
     const bool rdq = miss & (wr == 0u), req = miss | upg;
     const bool keep = miss & (dH == 0u) & !fwd;                 /* EM at the requester */
     const bool excl = !(rdq & (dH == 1u)) & !fwd;               /* REPLY_RD's bitVector == 2 */
-    const uint32_t nmemH = fwd ? vO : ((miss & (wr != 0u)) ? val : memH);
+    const uint32_t nmemH = (fwd & !dead) ? vO : ((miss & (wr != 0u)) ? val : memH);
     const uint32_t nbvH = rdq ? (dH == 2u ? bit : ((dH == 1u) | fwd ? (bvH | bit) : bvH)) : (keep ? bvH : bit);
     const uint32_t ndH = rdq ? (dH == 2u ? 0u : (fwd ? 1u : dH)) : 0u;
     /* write-back, branch-free (a disabled store goes to the dummy word); when the eviction's
@@ -502,9 +538,9 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
     m.st_if(ev & (vh != h), S_DS + vh, dsV2);
     m.st_if(ev & (wV != wH), wV, mbV2);
     /* the forward's owner: S after FLUSH, I after FLUSH_INVACK */
-    m.st_if(fwd, S_CT + o, (ctO & ~(3u << lsh)) | ((wr ? 3u : 2u) << lsh));
+    m.st_if(fwd & !dead, S_CT + o, (ctO & ~(3u << lsh)) | ((wr ? 3u : 2u) << lsh));
     /* the notice's target: its line (same index) S -> E when it still holds the victim */
-    if (notice) {
+    if (notice & !selfn) {
         const uint32_t laX = m.ld(S_LA + x), ctX = m.ld(S_CT + x);
         const bool up = (((laX >> sh8) & 0xFFu) == La) & (((ctX >> lsh) & 3u) == 2u);
         m.st_if(up, S_CT + x, (ctX & ~(3u << lsh)) | (1u << lsh));
@@ -520,12 +556,13 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
     }
     /* the requester's line (:243-246, :291-294, :445-447, :334-336, :491-494; a write hit
      * :642-643, :656-657), pendingWriteValue (:633), the instruction index */
-    const uint32_t nLv = fwd ? vO : (wr ? val : (miss ? memH : Lv));
-    const uint32_t nLs = wr ? 0u : (miss ? (excl ? 1u : 2u) : Ls);
+    const uint32_t nLv = dead ? 0u : (fwd ? vO : (wr ? val : (miss ? memH : Lv)));
+    const uint32_t nLs = dead ? 3u : (wr ? 0u : (miss ? (excl ? 1u : 2u) : Ls));
     const uint32_t nla = (laW & ~(0xFFu << sh8)) | (a << sh8);
     const uint32_t nlv = (lvW & ~(0xFFu << sh8)) | (nLv << sh8);
     ct = (ct & ~(3u << lsh)) | (nLs << lsh);
     ct = (wr ? ((ct & ~0xFFu) | val) : ct) + (1u << SC_IP);
+    ct |= dead ? (uint32_t)SC_WAIT : 0u;
     m.st(S_LA + n, nla);
     m.st(S_LV + n, nlv);
     m.st(S_CT + n, ct);
@@ -539,10 +576,15 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch) {
      * INVs. */
     const bool lone = hit & !upg;
     const uint32_t treq = (ev & (vh == h)) ? 3u : 2u;
-    r.rounds += lone ? 1u : treq + (fwd ? 2u : 1u);
-    r.msgs += lone ? 0u : (ev ? 1u : 0u) + (notice ? 1u : 0u) + 2u + (fwd ? (n != h ? 2u : 1u) : 0u) +
+    r.rounds += lone ? 1u : treq + ((fwd & !dead) ? 2u : 1u);
+    r.msgs += lone ? 0u : (ev ? 1u : 0u) + (notice ? 1u : 0u) + 2u + ((fwd & !dead) ? (n != h ? 2u : 1u) : 0u) +
                           (fan ? (uint32_t)__builtin_popcount(others) : 0u);
     r.E = 0u;
+    /* the dead end: the requester waits, no node can act after the owner's round -- the
+     * system is quiescent (the caller ends it when r.A is empty) */
+    r.iss = dead ? (r.iss & ~bit) : r.iss;
+    r.A = r.iss;
+    r.st = (r.dmp == NPM) ? SS_COMPLETED : SS_DEADLOCKED;
     return true;
 }
 

@@ -98,9 +98,9 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         do {
             /* as the kernel: a lone node's whole transaction at once when it applies */
             if (macro && cap >= 256u && dsms::ser_quiet_lone(r, lim)) {
-                if (dsms::ser_macro<NP>(m, r, cc, fetch_try)) {
+                if (dsms::ser_macro<NP>(m, r, cc, fetch_try, on_dump)) {
                     ++n_macro;
-                    v = dsms::SR_RUN;
+                    v = r.A ? dsms::SR_RUN : dsms::SR_DONE;     /* a dead-end forward ends it */
                     continue;
                 }
                 const uint32_t n0 = dsms::s_ctz(r.A);

@@ -69,3 +69,30 @@ def test_serial_engine_matches_oracle(serial_model, case):
         assert d["macro"] > (100 * d["systems"] if case[4] == 0 else 0), d
     elif not macro:
         assert d["macro"] == 0
+
+
+@pytest.fixture(scope="module")
+def serial_model_dump(tmp_path_factory):
+    """The build with the lone node's dump inside the macro-step (SER_DUMP=1: exact, not the
+    default -- measured slower on C5)."""
+    d = tmp_path_factory.mktemp("serd")
+    obj = str(d / "orc.o")
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-c", os.path.join(REPO, "oracle", "dsm_oracle.c"),
+                    "-I", os.path.join(REPO, "oracle"), "-o", obj], check=True)
+    exe = str(d / "serial_model")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fopenmp", "-DSER_DUMP=1",
+                    "-I", os.path.join(REPO, "oracle"),
+                    "-I", os.path.join(REPO, "hp-assignment-2_amd", "csrc"),
+                    os.path.join(REPO, "tests", "model", "serial_model.cpp"), obj, "-o", exe],
+                   check=True)
+    return exe
+
+
+@pytest.mark.parametrize("case", [(8, 0, 1000, 8, 0, 4096, 256), (8, 1, 300, 8, 0, 4096, 256),
+                                  (8, 2, 1000, 8, 0, 4096, 256)])
+def test_macro_dump_build_matches_oracle(serial_model_dump, case):
+    r = subprocess.run([serial_model_dump] + [str(x) for x in case], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["compared"] == d["systems"] and d["declined_dump"] == 0, d
