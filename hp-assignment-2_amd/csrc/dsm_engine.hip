@@ -1245,12 +1245,6 @@ constexpr int SER_MACRO = SER_MACRO_DEF;   /* lone-node macro-steps per iteratio
 /* SER_PROBE builds (diagnostics, never the default): per-wave event counts of the serial pass
  * in the counter slots the pass leaves unused (msgs_by_type 0-4): iterations, iterations with
  * a macro-step, with a one-action step, with a chunk miss, hand-overs */
-#ifndef SER_HDR_FIRST
-#define SER_HDR_FIRST 1
-#endif
-#ifndef SER_CLAIM_EARLY
-#define SER_CLAIM_EARLY 1
-#endif
 #ifndef SER_PROBE
 #define SER_PROBE 0
 #endif
@@ -1312,6 +1306,10 @@ ser_kernel(const SimArgs *Ap) {
                               (GU32 *)(Ap->spill + ((uint64_t)blockIdx.x * (64 * SER_WAVES) + threadIdx.x) * S_SPILL)};
     const LdsTab T{s_tab};
     const uint32_t n = *Ap->d_n;
+    /* claim k -> system: last-suspended first, as the lock-step resume (whose records are the
+     * likeliest still in the MALL; longest-first orders measured slower) */
+    const uint32_t *const list = Ap->list;
+    auto sel = [&](uint32_t k) -> uint32_t { return list[n - 1 - k]; };
     const uint32_t stride = Ap->stride, lim_rsh = Ap->lim_rsh, SR = Ap->susp_ring;
     const uint32_t cap = Ap->icap;
     const uint16_t *const traces = Ap->traces;
@@ -1319,7 +1317,6 @@ ser_kernel(const SimArgs *Ap) {
     /* uniform pointers, hoisted */
     uint4 *const recs = Ap->recs;
     dsm_sys_result *const results = Ap->results;
-    const uint32_t *const list = Ap->list;
     const uint32_t *const susp = Ap->susp;
     uint32_t *const ovf_list = Ap->ovf_list;
     unsigned int *const ovf_count = Ap->ovf_count, *const claim_ctr = Ap->claim;
@@ -1342,7 +1339,7 @@ ser_kernel(const SimArgs *Ap) {
     auto claim = [&]() -> bool {
         const uint32_t k = atomicAdd(claim_ctr, 1u);
         if (k >= n) return false;
-        sys = list[n - 1 - k];             /* last-suspended first, as the lock-step resume */
+        sys = sel(k);
         return true;
     };
     /* the state the budget pass suspended, in serial form (ssusp_words): the LDS column as
@@ -1399,12 +1396,6 @@ ser_kernel(const SimArgs *Ap) {
         } else {
         const GU32 *sp = (const GU32 *)(susp + sys * (uint64_t)ssusp_words((int)SR));
         const GV4 *sv = (const GV4 *)sp;
-        /* the header rows in flight with the first batch of the column's (SER_HDR_FIRST) */
-        v4u32 hd[9];
-        if (SER_HDR_FIRST) {
-#pragma unroll
-            for (uint32_t i = 0; i < 9; ++i) hd[i] = sv[24u + i];
-        }
 #pragma unroll
         for (uint32_t bt = 0; bt < 2; ++bt) {
             v4u32 x[12];
@@ -1416,10 +1407,9 @@ ser_kernel(const SimArgs *Ap) {
                 m.st(w, x[i].x); m.st(w + 1u, x[i].y); m.st(w + 2u, x[i].z); m.st(w + 3u, x[i].w);
             }
         }
-        if (!SER_HDR_FIRST) {
+        v4u32 hd[9];
 #pragma unroll
-            for (uint32_t i = 0; i < 9; ++i) hd[i] = sv[24u + i];
-        }
+        for (uint32_t i = 0; i < 9; ++i) hd[i] = sv[24u + i];
         r.rounds = hd[6].x;
         auto hw = [&](uint32_t k) -> uint32_t {        /* header word 96 + k, k < 24 (unrolled) */
             const v4u32 &v = hd[k >> 2];
@@ -1640,18 +1630,9 @@ ser_kernel(const SimArgs *Ap) {
             if (live && v != SR_RUN) {
                 uint64_t th0 = 0, th1 = 0, th2 = 0;
                 if (SER_PROBE >= 3) th0 = __builtin_amdgcn_s_memtime();
-                /* SER_CLAIM_EARLY: the claim's atomic is issued before the finished system's
-                 * records are written, so its round trip overlaps them */
-                uint32_t k = 0;
-                if (SER_CLAIM_EARLY && SER_PROBE < 3) k = atomicAdd(claim_ctr, 1u);
                 finish(v);
                 if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th1 = __builtin_amdgcn_s_memtime(); }
-                if (SER_CLAIM_EARLY && SER_PROBE < 3) {
-                    live = k < n;
-                    if (live) sys = list[n - 1 - k];
-                } else {
-                    live = claim();
-                }
+                live = claim();
                 if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th2 = __builtin_amdgcn_s_memtime(); }
                 v = live ? start() : SR_RUN;
                 if (SER_PROBE >= 3) {    /* hand-over cycles: finish, claim, start (lowest lane) */
@@ -1951,6 +1932,7 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     /* the budget pass checks for quiet-lone systems every DSM_LONE rounds (0: never) */
     c->lone_rounds = env_u32("DSM_LONE", 8);
     c->lone_min = env_u32("DSM_LONE_MIN", 256);
+
     c->fmt_tile = (int)env_u32("DSM_FMT", 132);
     c->parse_bpl = (int)env_u32("DSM_PARSE_BPL", 32);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -2157,6 +2139,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.thr_ff = (mode == 0) ? c->ff_budget_rounds : 0u;
     A.lone = (use_ser && (plain_only || pair)) ? c->lone_rounds : 0u;   /* serial resume only */
     A.lone_min = c->lone_min;
+
     /* the serial-form record and suspend-on-lone are compiled into the plain budget kernel
      * only (sim_kernel LONE): runs whose budget pass takes it, the pair's plain half or the
      * plain-only bench mode; with limits (M_LIM) the budget pass writes the lock-step form */
