@@ -721,15 +721,18 @@ sim_kernel(const SimArgs *Ap) {
                      * iteration (C4 runs hundreds of hits per node between misses, where the
                      * 8-wide window took one loop iteration per 8). */
                     if (FF_LONG && __ballot(k == 8u)) {
+                        /* chunks per scan step: generated chunks hide no latency and eight
+                         * unrolled generator calls spilled the fused kernel (103 VGPRs) */
+                        constexpr int LU = GEN ? 1 : FF_LONG_U;
                         lng = k == 8u;                                    /* group-uniform */
                         constexpr uint32_t INF = 0xFFFFFFFFu;
                         const uint32_t nl = nd.nins - nd.ip;
                         uint32_t found = iss ? (nl < rmax ? nl : rmax) : INF;
                         uint32_t cc = (nd.ip >> 3) + 1u;     /* its first unscanned positions */
                         bool go = lng;
-                        auto chunks = [&](uint32_t c, uint32_t (&w)[FF_LONG_U][4]) {
+                        auto chunks = [&](uint32_t c, uint32_t (&w)[LU][4]) {
     #pragma unroll
-                            for (int u = 0; u < FF_LONG_U; ++u) {
+                            for (int u = 0; u < LU; ++u) {
                                 if (GEN) {
                                     gen_chunk<NP>(gmul, gdist, gfirst + sys, node, c + u, w[u]);
                                 } else {
@@ -739,23 +742,23 @@ sim_kernel(const SimArgs *Ap) {
                                 }
                             }
                         };
-                        uint32_t wn[FF_LONG_U][4];       /* FF_LONG_PIPE: the next step's chunks */
+                        uint32_t wn[LU][4];       /* FF_LONG_PIPE: the next step's chunks */
                         if (FF_LONG_PIPE && go && iss) chunks(cc, wn);
                         while (__ballot(go)) {
                             if (go) {
                                 if (iss) {
-                                    uint32_t w[FF_LONG_U][4];
+                                    uint32_t w[LU][4];
                                     if (FF_LONG_PIPE) {
     #pragma unroll
-                                        for (int u = 0; u < FF_LONG_U; ++u)
+                                        for (int u = 0; u < LU; ++u)
     #pragma unroll
                                             for (int q = 0; q < 4; ++q) w[u][q] = wn[u][q];
-                                        chunks(cc + FF_LONG_U, wn);      /* in flight over this step */
+                                        chunks(cc + LU, wn);      /* in flight over this step */
                                     } else {
                                         chunks(cc, w);
                                     }
     #pragma unroll
-                                    for (int u = FF_LONG_U - 1; u >= 0; --u) {    /* the first miss wins */
+                                    for (int u = LU - 1; u >= 0; --u) {    /* the first miss wins */
                                         const uint32_t xa = misses(w[u][0], w[u][1]), xb = misses(w[u][2], w[u][3]);
                                         const uint32_t q = xa ? (uint32_t)__builtin_ctz(xa) >> 3
                                                               : (xb ? 4u + ((uint32_t)__builtin_ctz(xb) >> 3) : 8u);
@@ -764,9 +767,9 @@ sim_kernel(const SimArgs *Ap) {
                                     }
                                 }
                                 /* every node's run is at least its coverage unless found */
-                                const uint32_t gc = gmin<NP>(iss ? 8u * (cc + FF_LONG_U) - nd.ip : INF);
+                                const uint32_t gc = gmin<NP>(iss ? 8u * (cc + LU) - nd.ip : INF);
                                 go = gmin<NP>(found) > gc;
-                                cc += FF_LONG_U;
+                                cc += LU;
                             }
                         }
                         if (lng) k = gmin<NP>(found);
@@ -1585,7 +1588,22 @@ ser_kernel(const SimArgs *Ap) {
                         const uint32_t n0 = dsms::s_ctz(r.A), ip0 = m.ld(S_CT + n0) >> SC_IP, c0 = ip0 >> 3;
                         nohave = !((tn == n0) & ((tci == c0) | ((tci + 1u == c0) & nxv)));
                     }
-                    if (__ballot(q) && q) did = ser_macro<NP>(m, r, cc, fetch_reg, on_dump);
+                    if (SER_PROBE >= 4) {     /* phase cycles of the macro-step (lane 0's view) */
+                        uint64_t ts[5] = {0, 0, 0, 0, 0};
+                        auto stamp = [&](int i) { __builtin_amdgcn_s_waitcnt(0); ts[i + 1] = __builtin_amdgcn_s_memtime(); };
+                        __builtin_amdgcn_s_waitcnt(0);
+                        ts[0] = __builtin_amdgcn_s_memtime();
+                        if (__ballot(q) && q) did = ser_macro<NP>(m, r, cc, fetch_reg, on_dump, stamp);
+                        const uint64_t okb = __ballot(did);
+                        if (okb && lane == (uint32_t)__builtin_ctzll(okb)) {
+                            atomicAdd(&s_cnt[13], ts[1] - ts[0]);      /* entry + fetch      */
+                            atomicAdd(&s_cnt[14], ts[2] - ts[1]);      /* the homes' words   */
+                            atomicAdd(&s_cnt[15], ts[3] - ts[2]);      /* decide             */
+                            atomicAdd(&s_cnt[16], ts[4] - ts[3]);      /* write-back         */
+                        }
+                    } else if (__ballot(q) && q) {
+                        did = ser_macro<NP>(m, r, cc, fetch_reg, on_dump, [](int) {});
+                    }
                     if (SER_PROBE && j == 0) {
                         const uint64_t nh = __ballot(nohave);
                         if (lane == 0) atomicAdd(&s_cnt[8 + 3], 0ull + __builtin_popcountll(nh));

@@ -418,8 +418,10 @@ struct SCache {
 };
 DSM_HD void ser_cache_clear(SCache &c) { c.ct = c.la = c.lv = 0u; c.node = 0xFFu; }
 
-template <int NP, class M, class F, class R>
-DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump) {
+/* stamp(i): diagnostic hook (the kernel's SER_PROBE 4 build times the step's phases; else a
+ * no-op) */
+template <int NP, class M, class F, class R, class P>
+DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&stamp) {
     constexpr uint32_t NPM = (1u << NP) - 1u;
     const uint32_t n = s_ctz(r.A), bit = 1u << n;
     const bool hot = cc.node == n;
@@ -443,6 +445,7 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump) {
     }
     uint32_t ins;
     if (!fetch(n, ip, ins)) return false;                     /* not at hand: ser_step loads it */
+    stamp(0);
     const uint32_t a = (ins >> 8) & 0x7Fu, wr = ins >> 15, val = ins & 0xFFu;
     const uint32_t h = a >> 4, b = a & 15u, idx = a & 3u, sh8 = 8u * idx;
     const uint32_t laW = hot ? cc.la : m.ld(S_LA + n), lvW = hot ? cc.lv : m.ld(S_LV + n);
@@ -463,6 +466,7 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump) {
     /* the eviction at the victim's home (:498-561) */
     const uint32_t hv = 16u * (vb & 1u), sv = 2u * vb;
     const uint32_t memV = (mbV >> hv) & 0xFFu, bvV = (mbV >> (hv + 8u)) & 0xFFu, dV = (dsV >> sv) & 3u;
+    stamp(1);
     const bool mod = Ls == 0u;
     const bool had = (bvV & bit) != 0u;
     const uint32_t bvS = bvV & ~bit;                            /* EVICT_SHARED, bit set */
@@ -520,6 +524,7 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump) {
                     !(notice & ((((x == h) | (x == vh)) & !SER_NOTICE_HOME) | (fwd & (x == o)) |
                                 (fan & (((others >> x) & 1u) != 0u))));
     if (!ok) return false;
+    stamp(2);
     /* the home's directory entry and memory after the request (:188-236, :298-328, :375-435):
      * READ_REQUEST U -> EM {n}, S -> S + n, EM at n unchanged, EM at o -> S {o, n};
      * WRITE_REQUEST writes memory first, then U / S -> EM {n}, EM at n unchanged, EM at o ->
@@ -567,6 +572,7 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump) {
     m.st(S_LV + n, nlv);
     m.st(S_CT + n, ct);
     cc.ct = ct; cc.la = nla; cc.lv = nlv; cc.node = n;
+    stamp(3);
     /* rounds: the issue; the request's round (2, or 3 when the eviction queued before it at
      * the same home); a reply the round after -- or the forward's round, then the flush.
      * The INVs after a REPLY_ID are taken in the round after the reply, the round of the

@@ -53,7 +53,9 @@ for r in range(reps):
                   f"cycles macro {int(raw[5])} one-action {int(raw[6])} hand-over {int(raw[7])} "
                   f"live-lanes {int(raw[8])} lanes-not-quiet {int(raw[9])} lanes-quiet-declined {int(raw[10])} not-at-hand {int(raw[11])} "
                   f"iters-under-half-live {int(raw[12])} hand-over cycles finish / claim / start "
-                  f"{int(raw[13])} / {int(raw[14])} / {int(raw[15])} (SER_PROBE 3)", flush=True)
+                  f"{int(raw[13])} / {int(raw[14])} / {int(raw[15])} (SER_PROBE 3); macro-step phases "
+                  f"entry+fetch / homes' words / decide / write-back {int(raw[13])} / {int(raw[14])} / "
+                  f"{int(raw[15])} / {int(raw[16])} (SER_PROBE 4)", flush=True)
         info[v] = eng.launch_info()
 for v in variants:
     print(f"{var}={v} [{dist}, {n} systems]: kernel ms median {np.median(res[v]):.2f} "
