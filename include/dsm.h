@@ -266,7 +266,7 @@ int dsm_kernel_ms_history(dsm_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);
  * pass continues them -- in serial form, one system per lane (DSM_SERIAL=0 at dsm_open: the
  * lock-step resume), or, for traces the fast-forward verdict picks, the fast-forward
  * lock-step kernel (their budget pass: the plain kernel at the fast-forward budget).
- * Results never depend on it.  Defaults 12 / 9 (or DSM_BUDGET_LOG2 / DSM_LATE_LOG2 at
+ * Results never depend on it.  Defaults 12 / 0 (or DSM_BUDGET_LOG2 / DSM_LATE_LOG2 at
  * dsm_open); the fast-forward kernel's budget is 384 rounds (DSM_FF_BUDGET_ROUNDS, or
  * DSM_FF_BUDGET_LOG2 as a power of two; 0 = the plain budget). */
 int dsm_set_budget(dsm_ctx *ctx, uint32_t budget_log2, uint32_t late_log2);
