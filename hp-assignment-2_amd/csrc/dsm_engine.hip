@@ -1527,21 +1527,6 @@ ser_kernel(const SimArgs *Ap) {
         ins = (wd >> (16u * (j & 1u))) & 0xFFFFu;
         return have;
     };
-    /* the next transaction's instruction for the macro-step's read-ahead: from cur or nx as
-     * they are (no rotation, no load) */
-    auto peek_reg = [&](uint32_t nd, uint32_t ip, uint32_t &ins) -> bool {
-        const uint32_t c = ip >> 3;
-        const bool tnd = tn == nd;
-        const bool inc = tnd & (tci == c), innx = tnd & (tci + 1u == c) & nxv;
-        const uint32_t x0 = innx ? nx.x : cur.x, x1 = innx ? nx.y : cur.y;
-        const uint32_t x2 = innx ? nx.z : cur.z, x3 = innx ? nx.w : cur.w;
-        const uint32_t j = ip & 7u;
-        const uint32_t m2 = 0u - ((j >> 1) & 1u), m4 = 0u - ((j >> 2) & 1u);
-        const uint32_t lo = (x0 & ~m2) | (x1 & m2), hi = (x2 & ~m2) | (x3 & m2);
-        const uint32_t wd = (lo & ~m4) | (hi & m4);
-        ins = (wd >> (16u * (j & 1u))) & 0xFFFFu;
-        return inc | innx;
-    };
     auto refill = [&]() {
         /* pf (chunk pfc, issued at an earlier refill) becomes nx once cur reaches pfc - 1;
          * then the chunk after the newest one held or in flight is requested, so two chunks
@@ -1608,7 +1593,7 @@ ser_kernel(const SimArgs *Ap) {
                         auto stamp = [&](int i) { __builtin_amdgcn_s_waitcnt(0); ts[i + 1] = __builtin_amdgcn_s_memtime(); };
                         __builtin_amdgcn_s_waitcnt(0);
                         ts[0] = __builtin_amdgcn_s_memtime();
-                        if (__ballot(q) && q) did = ser_macro<NP>(m, r, cc, fetch_reg, on_dump, stamp, peek_reg);
+                        if (__ballot(q) && q) did = ser_macro<NP>(m, r, cc, fetch_reg, on_dump, stamp);
                         const uint64_t okb = __ballot(did);
                         if (okb && lane == (uint32_t)__builtin_ctzll(okb)) {
                             atomicAdd(&s_cnt[13], ts[1] - ts[0]);      /* entry + fetch      */
@@ -1617,7 +1602,7 @@ ser_kernel(const SimArgs *Ap) {
                             atomicAdd(&s_cnt[16], ts[4] - ts[3]);      /* write-back         */
                         }
                     } else if (__ballot(q) && q) {
-                        did = ser_macro<NP>(m, r, cc, fetch_reg, on_dump, [](int) {}, peek_reg);
+                        did = ser_macro<NP>(m, r, cc, fetch_reg, on_dump, [](int) {});
                     }
                     if (SER_PROBE && j == 0) {
                         const uint64_t nh = __ballot(nohave);

@@ -53,9 +53,6 @@
 #ifndef SER_NOTICE_HOME
 #define SER_NOTICE_HOME 1   /* ... and an upgrade notice to either home */
 #endif
-#ifndef SER_PF_NEXT
-#define SER_PF_NEXT 0       /* ... with the next transaction's home words read ahead */
-#endif
 #ifndef SER_DUMP
 #define SER_DUMP 0          /* ... and the lone node's dump (exact, but C5 33.4 vs 32.5 ms: off) */
 #endif
@@ -418,21 +415,13 @@ DSM_HD bool ser_quiet_lone(const SReg &r, uint32_t lim_rsh) {
  * action of a system between two of them (ser_step or a hand-over invalidates the cache) */
 struct SCache {
     uint32_t ct, la, lv, node;      /* node: the node they belong to, 0xFF: none */
-    /* SER_PF_NEXT: the four home words of the node's next transaction (instruction pip),
-     * read at the end of this one -- nothing else writes the column before that step */
-    uint32_t pip, pmbV, pdsV, pmbH, pdsH;
 };
-DSM_HD void ser_cache_clear(SCache &c) {
-    c.ct = c.la = c.lv = 0u;
-    c.node = 0xFFu;
-    c.pip = 0xFFFFFFFFu;
-    c.pmbV = c.pdsV = c.pmbH = c.pdsH = 0u;
-}
+DSM_HD void ser_cache_clear(SCache &c) { c.ct = c.la = c.lv = 0u; c.node = 0xFFu; }
 
 /* stamp(i): diagnostic hook (the kernel's SER_PROBE 4 build times the step's phases; else a
  * no-op) */
-template <int NP, class M, class F, class R, class P, class K>
-DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&stamp, K &&peek) {
+template <int NP, class M, class F, class R, class P>
+DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&stamp) {
     constexpr uint32_t NPM = (1u << NP) - 1u;
     const uint32_t n = s_ctz(r.A), bit = 1u << n;
     const bool hot = cc.node == n;
@@ -472,13 +461,8 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&sta
      * victim's line has the same index as the request's (it is the line being replaced). */
     const uint32_t vh = (La >> 4) & 7u, vb = La & 15u;
     const uint32_t wV = S_MB + 8u * vh + (vb >> 1), wH = S_MB + 8u * h + (b >> 1);
-    uint32_t mbV, dsV, mbH0, dsH0;
-    if (SER_PF_NEXT && hot && cc.pip == ip) {          /* read at the end of the last step */
-        mbV = cc.pmbV; dsV = cc.pdsV; mbH0 = cc.pmbH; dsH0 = cc.pdsH;
-    } else {
-        mbV = m.ld(wV); dsV = m.ld(S_DS + vh);
-        mbH0 = m.ld(wH); dsH0 = m.ld(S_DS + h);
-    }
+    const uint32_t mbV = m.ld(wV), dsV = m.ld(S_DS + vh);
+    const uint32_t mbH0 = m.ld(wH), dsH0 = m.ld(S_DS + h);
     /* the eviction at the victim's home (:498-561) */
     const uint32_t hv = 16u * (vb & 1u), sv = 2u * vb;
     const uint32_t memV = (mbV >> hv) & 0xFFu, bvV = (mbV >> (hv + 8u)) & 0xFFu, dV = (dsV >> sv) & 3u;
@@ -588,20 +572,6 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&sta
     m.st(S_LV + n, nlv);
     m.st(S_CT + n, ct);
     cc.ct = ct; cc.la = nla; cc.lv = nlv; cc.node = n;
-    cc.pip = 0xFFFFFFFFu;
-    if (SER_PF_NEXT && !dead) {      /* the next transaction's home words, in flight meanwhile */
-        uint32_t ins2 = 0;
-        if (ip + 1u < s_ni(r, n) && peek(n, ip + 1u, ins2)) {
-            const uint32_t a2 = (ins2 >> 8) & 0x7Fu, h2 = a2 >> 4, b2 = a2 & 15u;
-            const uint32_t La2 = (nla >> (8u * (a2 & 3u))) & 0xFFu;
-            const uint32_t vh2 = (La2 >> 4) & 7u, vb2 = La2 & 15u;
-            cc.pmbV = m.ld(S_MB + 8u * vh2 + (vb2 >> 1));
-            cc.pdsV = m.ld(S_DS + vh2);
-            cc.pmbH = m.ld(S_MB + 8u * h2 + (b2 >> 1));
-            cc.pdsH = m.ld(S_DS + h2);
-            cc.pip = ip + 1u;
-        }
-    }
     stamp(3);
     /* rounds: the issue; the request's round (2, or 3 when the eviction queued before it at
      * the same home); a reply the round after -- or the forward's round, then the flush.

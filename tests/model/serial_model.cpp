@@ -98,7 +98,7 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         do {
             /* as the kernel: a lone node's whole transaction at once when it applies */
             if (macro && cap >= 256u && dsms::ser_quiet_lone(r, lim)) {
-                if (dsms::ser_macro<NP>(m, r, cc, fetch_try, on_dump, [](int) {}, fetch_try)) {
+                if (dsms::ser_macro<NP>(m, r, cc, fetch_try, on_dump, [](int) {})) {
                     ++n_macro;
                     v = r.A ? dsms::SR_RUN : dsms::SR_DONE;     /* a dead-end forward ends it */
                     continue;
