@@ -268,9 +268,6 @@ DEVI uint32_t lowmask(uint32_t n) { return n >= 32u ? 0xFFFFFFFFu : (1u << n) - 
 #ifndef PARSE_OCC
 #define PARSE_OCC 6
 #endif
-#ifndef PARSE_PRED
-#define PARSE_PRED 0        /* the chunk loop's body predicated instead of behind a branch */
-#endif
 #ifndef PARSE_UNROLL
 #define PARSE_UNROLL 0      /* the chunk loop's first 4 chunks per lane in two fixed rounds */
 #endif
@@ -405,25 +402,6 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
             }
 #endif
             while (__ballot((mcs != 0u) & (t < tmax))) {
-#if PARSE_PRED
-                /* predicated: every lane decodes (a lane without a chunk reads its own bytes at
-                 * offset 31; the VALU cost is the wave's either way), only the store and the
-                 * slow mark are masked -- no exec-mask branch around the body */
-                {
-                    const bool act = (mcs != 0u) & (t < tmax);
-                    const uint32_t b = (uint32_t)__builtin_ctz(mcs | 0x80000000u), o = BPL * lane + b;
-                    const uint32_t lim = rem - o < DP_CHUNK ? rem - o : DP_CHUNK;
-                    const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
-                    const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
-                    const uint32_t c0 = __builtin_amdgcn_alignbyte(d1, d0, o & 3u);
-                    const uint32_t c1 = __builtin_amdgcn_alignbyte(d2, d1, o & 3u);
-                    const uint32_t c2 = __builtin_amdgcn_alignbyte(d3, d2, o & 3u);
-                    uint32_t pk = 0;
-                    const bool ok = parse_fast(c0, c1, c2, lim, &pk) & (((pk >> 12) & 7u) < (uint32_t)np);
-                    if (act & ok) out[idx0 + t] = (uint16_t)pk;
-                    slow |= (act & !ok) ? 1u << b : 0u;
-                }
-#else
                 if ((mcs != 0u) & (t < tmax)) {
                     const uint32_t b = (uint32_t)__builtin_ctz(mcs), o = BPL * lane + b;
                     const uint32_t lim = rem - o < DP_CHUNK ? rem - o : DP_CHUNK;
@@ -437,7 +415,6 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
                     if (ok) out[idx0 + t] = (uint16_t)pk;
                     slow |= ok ? 0u : 1u << b;
                 }
-#endif
                 mcs &= mcs - 1u;
                 ++t;
             }
