@@ -110,9 +110,6 @@ struct SimArgsPack { SimArgs a[3]; };
 #ifndef FF_LONG_U
 #define FF_LONG_U 8         /* trace chunks per step of that scan (hot, C4: 1 / 2 / 4 / 6 / 8 -> 49.6 / 39.3 / 34.1 / 32.6 / 32.1 ms) */
 #endif
-#ifndef FF_LONG_PIPE
-#define FF_LONG_PIPE 0      /* ... with the next step's chunks loaded during this one */
-#endif
 
 namespace {
 
@@ -742,21 +739,11 @@ sim_kernel(const SimArgs *Ap) {
                                 }
                             }
                         };
-                        uint32_t wn[LU][4];       /* FF_LONG_PIPE: the next step's chunks */
-                        if (FF_LONG_PIPE && go && iss) chunks(cc, wn);
                         while (__ballot(go)) {
                             if (go) {
                                 if (iss) {
                                     uint32_t w[LU][4];
-                                    if (FF_LONG_PIPE) {
-    #pragma unroll
-                                        for (int u = 0; u < LU; ++u)
-    #pragma unroll
-                                            for (int q = 0; q < 4; ++q) w[u][q] = wn[u][q];
-                                        chunks(cc + LU, wn);      /* in flight over this step */
-                                    } else {
-                                        chunks(cc, w);
-                                    }
+                                    chunks(cc, w);
     #pragma unroll
                                     for (int u = LU - 1; u >= 0; --u) {    /* the first miss wins */
                                         const uint32_t xa = misses(w[u][0], w[u][1]), xb = misses(w[u][2], w[u][3]);
