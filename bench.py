@@ -540,7 +540,7 @@ def main():
         roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
                     kernel=(("sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain) budget pass "
-                             "(the fast-forward budget, 384 rounds by default) + sim_kernel<8, 12, 4, false, 0, 5> resume "
+                             "(the fast-forward budget, 448 rounds by default) + sim_kernel<8, 12, 4, false, 0, 5> resume "
                              "pass with the hit-run fast-forward; 4-wave groups, ring 12, packed traces; the pair picked per "
                              "run by ffscan_kernel's trace sample")
                             if ff_picked and launches == 2 and not args.fused else

@@ -1927,7 +1927,7 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->ff_budget_log2 = env_u32("DSM_FF_BUDGET_LOG2", 0);
     if (c->ff_budget_log2 >= RSH_MAX) c->ff_budget_log2 = 0;
     c->ff_budget_rounds = getenv("DSM_FF_BUDGET_LOG2") ? (c->ff_budget_log2 ? 1u << c->ff_budget_log2 : 0u)
-                                                       : env_u32("DSM_FF_BUDGET_ROUNDS", 384);
+                                                       : env_u32("DSM_FF_BUDGET_ROUNDS", 448);
     if (c->ff_budget_rounds >= (1u << RSH_MAX)) c->ff_budget_rounds = 0;
     /* the late budget (a shorter budget once a wave finds no new system) is off: with
      * suspend-on-lone it only cut multi-node systems short into the serial pass, where they
@@ -2142,7 +2142,8 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
      * wave in the same phase, so the groups enter and leave fast-forward mode together and
      * the normal round is skipped more often (measured on C4, budget 256 / 320 / 384 / 416 /
      * 512 / 640 / 1024 / 2048 rounds: 50.9 / 48.7 / 48.3 / 48.4 / 49.0 / 50.0 / 53.4 /
-     * 57.7 ms).  Bench mode only: with a round or inbox limit (M_LIM) the kernel always has
+     * 57.7 ms; round 4, with the long runs: 320 / 384 / 416 / 448 / 480 / 512 / 640: 34.8 /
+     * 32.2 / 31.3 / 31.0 / 30.9 / 31.2 / 33.9 ms).  Bench mode only: with a round or inbox limit (M_LIM) the kernel always has
      * the fast-forward step and takes the plain budget. */
     A.budget = blog ? 1u : 0u;
     A.thr_ff = (mode == 0) ? c->ff_budget_rounds : 0u;

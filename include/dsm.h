@@ -178,7 +178,7 @@ typedef struct dsm_launch_info {
      * dsm_launch_info_get waits for the last run's stream to read its verdict. */
     int resume_form;       /* DSM_RESUME_*: the resume pass that ran                        */
     int budget_rounds;     /* the budget pass's effective budget in rounds (0: one pass):
-                            * 1 << budget_log2, or the fast-forward budget (384) when the
+                            * 1 << budget_log2, or the fast-forward budget (448) when the
                             * scan picked the hit-run fast-forward                           */
     int ff_picked;         /* 1 when the hit-run fast-forward kernel carried the run        */
 } dsm_launch_info;
@@ -267,7 +267,7 @@ int dsm_kernel_ms_history(dsm_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);
  * lock-step resume), or, for traces the fast-forward verdict picks, the fast-forward
  * lock-step kernel (their budget pass: the plain kernel at the fast-forward budget).
  * Results never depend on it.  Defaults 12 / 0 (or DSM_BUDGET_LOG2 / DSM_LATE_LOG2 at
- * dsm_open); the fast-forward kernel's budget is 384 rounds (DSM_FF_BUDGET_ROUNDS, or
+ * dsm_open); the fast-forward kernel's budget is 448 rounds (DSM_FF_BUDGET_ROUNDS, or
  * DSM_FF_BUDGET_LOG2 as a power of two; 0 = the plain budget). */
 int dsm_set_budget(dsm_ctx *ctx, uint32_t budget_log2, uint32_t late_log2);
 /* Round limit of the following runs: a system still active after 1 << limit_log2 rounds

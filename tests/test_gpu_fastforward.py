@@ -60,7 +60,7 @@ def test_packed_fast_forward_vs_oracle(dsm, orc, np_, dist, ring):
         assert cnt["ff_passes"] > 0 and cnt["ff_steps"] > 0
         # the trace scan picked the fast-forward pair: its kernel ran both passes' resume
         assert info["ff_picked"] == 1 and info["resume_form"] == 3, info
-        assert info["resume_blocks"] == info["grid_blocks"] and info["budget_rounds"] == 384, info
+        assert info["resume_blocks"] == info["grid_blocks"] and info["budget_rounds"] == 448, info
     else:
         assert info["ff_picked"] == 0 and info["resume_form"] == 2, info
 

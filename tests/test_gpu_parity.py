@@ -247,7 +247,7 @@ def test_full_size_1m_random(dsm, orc):
 @pytest.mark.parametrize("dist,n", [("hot", 1 << 20), ("evict", 1 << 21)])
 def test_full_size_c4_c5(dsm, orc, dist, n):
     """C4 (1M hot-line systems: the plain budget pass, then the fast-forward resume; every system
-    suspended at its 384-round budget) and C5 (2M eviction-heavy systems: budget pass + serial
+    suspended at its 448-round budget) and C5 (2M eviction-heavy systems: budget pass + serial
     resume) at full size, traces resident in HBM: per-system results and the aggregate
     counters equal the oracle over every system."""
     import torch
