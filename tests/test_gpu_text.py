@@ -250,3 +250,33 @@ def test_gpu_text_generator_round_trip(dsm, torch, dist):
         t = txt.cpu().numpy()
         files = [bytes(t[o[f]:o[f + 1]]) for f in (0, 1, 777, n_sys * 8 - 1)]
         assert all(fl.startswith((b"RD 0x", b"WR 0x")) and fl.endswith(b"\n") for fl in files)
+
+
+# valid lines longer than fgets' 19 bytes: each 19-byte chunk is a whole instruction
+LONG_OK = [b"RD 0x11" + b" " * 12 + b"RD 0x05\n",
+           b"WR 0x12 100" + b" " * 8 + b"WR 0x3f 7\n",
+           b"RD 0x01" + b" " * 12 + b"RD 0x02" + b" " * 12 + b"RD 0x03\n"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rate", [0.0005, 0.01, 0.2])
+def test_gpu_parse_sparse_long_lines_equal_host_reader(dsm, tmp_path, rate):
+    """Multi-window files whose valid long lines come at random, sparse to dense: windows with
+    and without a long line alternate, so both the line-start shortcut and the exact chunk
+    numbering (parse_kernel, :802-818 fgets(line, 20)) run and hand over line starts."""
+    rng = np.random.default_rng(int(rate * 1e4))
+    good = LINES[:6]
+    files = []
+    for _ in range(48):
+        k = int(rng.integers(200, 1500))
+        pick = [LONG_OK[int(rng.integers(0, 3))] if rng.random() < rate else good[int(rng.integers(0, 6))]
+                for _ in range(k)]
+        files.append(b"".join(pick))
+    cap = 4096
+    exp = _host_expect(dsm, tmp_path, files, 8, cap)
+    with dsm.Engine(8, cap) as eng:
+        tr, cn, st = eng.parse_traces(files, cap)
+    tr, cn, st = tr.reshape(len(files), -1), cn.reshape(-1), st.reshape(-1)
+    for f, (n, rc, t) in enumerate(exp):
+        assert (int(cn[f]), int(st[f])) == (n, rc), f
+        assert np.array_equal(tr[f, :n], t), f
