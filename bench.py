@@ -56,7 +56,7 @@ def shard(rank, n_per_rank):
 
 
 def reduce_counters(vec, dist_mod=None):
-    """All-reduce a 32-entry uint64 counter vector across ranks: sums (mod 2^64) for every
+    """All-reduce a dsm_counters vector (DSM_NCOUNTERS uint64) across ranks: sums (mod 2^64) for every
     slot except max_rounds (slot 24), which is a max.  `vec` is a torch int64 tensor."""
     return reduce_vector(vec, dist_mod, (24,))
 
@@ -387,7 +387,7 @@ def main():
     sp = stream.cuda_stream
 
     eng = pydsm.Engine(NP, n_instr, ring_cap=args.ring, device=local, timing=True)
-    cnt = torch.zeros(32, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device=dev)
     out = torch.empty((n_sys, 4), dtype=torch.int64, device=dev)
 
     trace_stream = None
@@ -537,18 +537,16 @@ def main():
         # back by dsm_launch_info_get) and which resume pass followed the budget pass
         ff_picked = li.get("ff_picked") == 1 or args.fused
         serial = li.get("resume_form") == 2
+        # the kernels that did the step's work, as the runtime launched them (the pair's picked
+        # halves; dsm_launch_kernel_names), e.g. "budget=sim_kernel<8, 12, 4, false, 48, 5>
+        # resume=ser_kernel<8, false>"
         roof = dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 6), traffic=None,
-                    kernel=(("sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain) budget pass "
-                             "(the fast-forward budget, 448 rounds by default) + sim_kernel<8, 12, 4, false, 0, 5> resume "
-                             "pass with the hit-run fast-forward; 4-wave groups, ring 12, packed traces; the pair picked per "
-                             "run by ffscan_kernel's trace sample")
-                            if ff_picked and launches == 2 and not args.fused else
-                            ("sim_kernel<8, 12, 4, false, 0, 5> (lock-step transition kernel with the hit-run fast-forward"
-                             if ff_picked else "sim_kernel<8, 12, 4, false, 16, 5> (lock-step transition kernel, plain")
-                            + "; 4-wave groups, ring 12, packed traces; picked per run by ffscan_kernel's trace sample)"
-                            + (f"; budget pass ({li['budget_rounds']} rounds) + resume pass" if launches == 2 else "")
-                            + (" in serial form (ser_kernel<8>: one lane per suspended system)" if serial else "")),
+                    kernel=li["kernels"] + (" (fused generator" if args.fused else " (packed traces")
+                    + (f"; budget pass {li['budget_rounds']} rounds" if launches == 2 else "")
+                    + ("; resume in serial form, one lane per suspended system" if serial else
+                       "; resume with the hit-run fast-forward" if ff_picked and launches == 2 else "")
+                    + ")",
                     launches_per_step=launches,
                     algorithmic_bytes_per_launch=alg_bytes, kernel_ms_avg=round(kavg, 3),
                     per_unit="2 B per consumed packed instruction + 32 B result + 4*np B counts per system"
@@ -639,13 +637,13 @@ def main():
             "counters": {k: c[k] for k in ("msgs", "instrs", "rounds", "systems", "max_rounds",
                                            "overflow_reruns", "wave_rounds", "resumed",
                                            "ff_passes", "ff_steps", "ff_sample_instrs",
-                                           "ff_sample_runs", "status_COMPLETED",
+                                           "ff_sample_runs", "ser_macro_steps", "status_COMPLETED",
                                            "status_DEADLOCKED")},
             "kernel_ms": [round(x, 3) for x in kms],
             "sum_final_hash": hex(c["sum_final_hash"]),
             "parity": parity,
             "parity_detail": parity_detail,
-            "collective": (("rccl" if backend == "nccl" else backend) + f" all_reduce of 32 counters over {world} rank(s)")
+            "collective": (("rccl" if backend == "nccl" else backend) + f" all_reduce of {pydsm.NCOUNTERS} counters over {world} rank(s)")
                           if use_dist else None,
             "launch": eng.launch_info(),
         }

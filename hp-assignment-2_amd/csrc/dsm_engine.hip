@@ -31,6 +31,7 @@
 #include <type_traits>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -128,7 +129,9 @@ constexpr uint32_t C_WAIT = DT_CTL_WAIT, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C
 /* counter slots (dsm_counters order) */
 enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
        K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_RESUMED = 27,
-       K_FFPASS = 28, K_FFITER = 29, K_SCANI = 30, K_SCANR = 31, K_N = 32 };
+       K_FFPASS = 28, K_FFITER = 29, K_SCANI = 30, K_SCANR = 31, K_N = 32,
+       K_SERMAC = 32 /* ser_kernel only, added straight to the device counters */ };
+static_assert(sizeof(dsm_counters) == DSM_NCOUNTERS * 8 && K_SERMAC < DSM_NCOUNTERS, "dsm_counters slots");
 constexpr uint32_t RSH_MAX = 22;    /* 1 << 22 == DSM_MAX_ROUNDS */
 static_assert((1u << RSH_MAX) == DSM_MAX_ROUNDS, "DSM_MAX_ROUNDS");
 /* suspended node state: memory/bitVector (8), lines (4), ring (RING), dst, ctl, ip, nins, rh,
@@ -1666,7 +1669,11 @@ ser_kernel(const SimArgs *Ap) {
         if (__ballot(live) == 0) break;
     }
     if (lane == 0) atomicAdd(&s_cnt[K_WROUNDS], (unsigned long long)iters);
-    if (!CAP && nmac) atomicAdd(&s_cnt[K_FFPASS], (unsigned long long)nmac);   /* multi-round steps */
+    if (!CAP) {          /* lone-node transaction steps (ser_macro): one atomic per wave */
+        uint32_t t = nmac;
+        for (int o = 1; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+        if (lane == 0 && t) atomicAdd(&Ap->counters[K_SERMAC], (unsigned long long)t);
+    }
     __syncthreads();
     if (threadIdx.x < K_N) {
         const unsigned long long x = s_cnt[threadIdx.x];
@@ -2004,11 +2011,40 @@ extern "C" int dsm_launch_info_get(dsm_ctx *c, dsm_launch_info *info) {
                                      : (c->last_use_ser ? DSM_RESUME_SERIAL : DSM_RESUME_LOCKSTEP);
             c->info.resume_blocks = (ff || !c->last_use_ser) ? c->last_grid_fast : c->last_ser_blocks;
             c->info.budget_rounds = (int)((ff && c->last_thr_ff) ? c->last_thr_ff : 1u << c->last_blog);
+            /* the budget pass runs on a plain kernel: with the serial resume, the M_SERB one
+             * unless the verdict picked the fast-forward resume (SimArgs::split) */
+            c->info.budget_mode = (!ff && c->last_use_ser) ? (M_NOFF | M_SERB) : M_NOFF;
+            c->info.resume_mode = ff ? 0 : (c->last_use_ser ? -1 : M_NOFF);
+        } else {
+            c->info.budget_mode = ff ? 0 : M_NOFF;
+            c->info.resume_mode = -1;
         }
         c->last_pair = 0;
     }
     *info = c->info;
     return DSM_OK;
+}
+
+extern "C" int dsm_launch_kernel_names(const dsm_launch_info *info, char *buf, size_t cap) {
+    if (!info || !buf) return DSM_E_INVAL;
+    char b[2][96];
+    auto sim = [&](char *o, int m) {
+        snprintf(o, 96, "sim_kernel<%d, %d, %d, %s, %d, %d>", info->np, info->ring_cap,
+                 info->block_threads / 64, info->gen ? "true" : "false", m, info->occ);
+    };
+    int n;
+    if (info->budget_mode < 0) {
+        n = snprintf(buf, cap, "none");
+    } else if (info->resume_form == DSM_RESUME_NONE) {
+        sim(b[0], info->budget_mode);
+        n = snprintf(buf, cap, "run=%s", b[0]);
+    } else {
+        sim(b[0], info->budget_mode);
+        if (info->resume_mode >= 0) sim(b[1], info->resume_mode);
+        else snprintf(b[1], 96, "ser_kernel<%d, %s>", info->np, info->ser_cap ? "true" : "false");
+        n = snprintf(buf, cap, "budget=%s resume=%s", b[0], b[1]);
+    }
+    return (n < 0 || (size_t)n >= cap) ? DSM_E_INVAL : n;
 }
 
 extern "C" int dsm_set_budget(dsm_ctx *c, uint32_t budget_log2, uint32_t late_log2) {
@@ -2046,6 +2082,7 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
         c->last_pair = 0;
         c->info.grid_blocks = c->info.block_threads = c->info.resume_blocks = 0;
         c->info.budget_log2 = c->info.late_log2 = c->info.budget_rounds = c->info.ff_picked = 0;
+        c->info.budget_mode = c->info.resume_mode = -1;
         c->info.resume_form = DSM_RESUME_NONE;
         return DSM_OK;
     }
@@ -2264,6 +2301,17 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
                         : use_ser ? DSM_RESUME_SERIAL
                         : (ff_kernel ? DSM_RESUME_FASTFORWARD : DSM_RESUME_LOCKSTEP);
     c->info.budget_rounds = blog ? (int)((ff_kernel && A.thr_ff) ? A.thr_ff : 1u << blog) : 0;
+    {   /* the MODE of `fast` as instantiated (fast_np_gen: the fused generator has no plain
+         * kernel); with the pair, dsm_launch_info_get replaces these with the picked halves */
+        const int fm = plain_only ? plain_mode : mode;
+        const int fmode = (gen && (fm & M_NOFF)) ? 0 : fm;
+        c->info.budget_mode = fmode;
+        c->info.resume_mode = (blog && !use_ser) ? fmode : -1;
+    }
+    c->info.np = np;
+    c->info.gen = gen ? 1 : 0;
+    c->info.occ = 5;                 /* sim_kernel's default OCC, every fast instantiation */
+    c->info.ser_cap = (use_ser && c->inbox_limit < (uint32_t)FB_RING) ? 1 : 0;
     c->last_st = st;
     c->last_pair = pair ? 1 : 0;
     c->last_use_ser = use_ser ? 1 : 0;

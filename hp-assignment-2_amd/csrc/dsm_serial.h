@@ -534,7 +534,7 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&sta
     const bool keep = miss & (dH == 0u) & !fwd;                 /* EM at the requester */
     const bool excl = !(rdq & (dH == 1u)) & !fwd;               /* REPLY_RD's bitVector == 2 */
     const uint32_t nmemH = (fwd & !dead) ? vO : ((miss & (wr != 0u)) ? val : memH);
-    const uint32_t nbvH = rdq ? (dH == 2u ? bit : ((dH == 1u) | fwd ? (bvH | bit) : bvH)) : (keep ? bvH : bit);
+    const uint32_t nbvH = rdq ? (dH == 2u ? bit : (((dH == 1u) | fwd) ? (bvH | bit) : bvH)) : (keep ? bvH : bit);
     const uint32_t ndH = rdq ? (dH == 2u ? 0u : (fwd ? 1u : dH)) : 0u;
     /* write-back, branch-free (a disabled store goes to the dummy word); when the eviction's
      * and the request's words coincide the request's write holds both */

@@ -33,8 +33,11 @@ COUNTER_FIELDS = ([f"msgs_{t}" for t in TYPE_NAMES] +
                   [f"status_{s}" for s in STATUS_NAMES] +
                   ["sum_dump_hash", "sum_final_hash", "max_rounds", "overflow_reruns",
                    "wave_rounds", "resumed", "ff_passes", "ff_steps", "ff_sample_instrs",
-                   "ff_sample_runs"])
-assert len(COUNTER_FIELDS) == 32
+                   "ff_sample_runs", "ser_macro_steps"] +
+                  [f"reserved_{i}" for i in range(7)])
+NCOUNTERS = 40                               # DSM_NCOUNTERS (ABI 4)
+assert len(COUNTER_FIELDS) == NCOUNTERS
+MAX_SLOT = COUNTER_FIELDS.index("max_rounds")   # the one counter that is a max, not a sum
 
 DUMP_BASE, DUMP_MAX, DUMP_SLOT = 1954, 1958, 1968
 VIEW_DUMP, VIEW_FINAL = 0, 1
@@ -64,7 +67,9 @@ class LaunchInfo(ctypes.Structure):
                 ("late_log2", ctypes.c_int), ("round_limit_log2", ctypes.c_int),
                 ("fmt_tile", ctypes.c_int), ("parse_bpl", ctypes.c_int),
                 ("resume_form", ctypes.c_int), ("budget_rounds", ctypes.c_int),
-                ("ff_picked", ctypes.c_int)]
+                ("ff_picked", ctypes.c_int), ("np", ctypes.c_int), ("gen", ctypes.c_int),
+                ("occ", ctypes.c_int), ("budget_mode", ctypes.c_int),
+                ("resume_mode", ctypes.c_int), ("ser_cap", ctypes.c_int)]
 
 
 RESUME_FORMS = {0: "none", 1: "lock-step", 2: "serial", 3: "fast-forward lock-step"}
@@ -95,6 +100,8 @@ def lib():
             "dsm_open": (i32, [i32, ctypes.POINTER(Config), ctypes.POINTER(vp)]),
             "dsm_close": (None, [vp]),
             "dsm_launch_info_get": (i32, [vp, ctypes.POINTER(LaunchInfo)]),
+            "dsm_launch_kernel_names": (i32, [ctypes.POINTER(LaunchInfo), ctypes.c_char_p,
+                                              ctypes.c_size_t]),
             "dsm_run_packed": (i32, [vp, vp, vp, u64, vp, vp]),
             "dsm_run_packed_device": (i32, [vp, vp, vp, u64, vp, vp, vp]),
             "dsm_generate_device": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp, vp]),
@@ -197,7 +204,7 @@ class Engine:
         assert traces.shape == (n, self.np, self.max_instr), traces.shape
         assert counts.shape == (n, self.np)
         res = np.zeros(n, dtype=RESULT_DTYPE)
-        cnt = np.zeros(32, dtype=np.uint64)
+        cnt = np.zeros(NCOUNTERS, dtype=np.uint64)
         _check(lib().dsm_run_packed(self.ctx, _ptr(traces), _ptr(counts), n, _ptr(res), _ptr(cnt)),
                "dsm_run_packed")
         return res, counters_to_dict(cnt)
@@ -205,7 +212,7 @@ class Engine:
     def run_generated(self, dist, seed, n_instr, first_sys, n_sys):
         g = Gen(seed, DIST.get(dist, dist), n_instr)
         res = np.zeros(n_sys, dtype=RESULT_DTYPE)
-        cnt = np.zeros(32, dtype=np.uint64)
+        cnt = np.zeros(NCOUNTERS, dtype=np.uint64)
         _check(lib().dsm_run_generated(self.ctx, ctypes.byref(g), first_sys, n_sys, _ptr(res),
                                        _ptr(cnt)), "dsm_run_generated")
         return res, counters_to_dict(cnt)
@@ -325,9 +332,18 @@ class Engine:
         _check(lib().dsm_set_fast_forward(self.ctx, mode), "dsm_set_fast_forward")
 
     def launch_info(self):
+        """dsm_launch_info of the last run, plus `kernels`: the kernels that did its work
+        (dsm_launch_kernel_names, e.g. "budget=sim_kernel<8, 12, 4, false, 48, 5>
+        resume=ser_kernel<8, false>")."""
         li = LaunchInfo()
         _check(lib().dsm_launch_info_get(self.ctx, ctypes.byref(li)), "dsm_launch_info_get")
-        return {k: getattr(li, k) for k, _ in LaunchInfo._fields_}
+        d = {k: getattr(li, k) for k, _ in LaunchInfo._fields_}
+        buf = ctypes.create_string_buffer(256)
+        n = lib().dsm_launch_kernel_names(ctypes.byref(li), buf, 256)
+        if n < 0:
+            raise DsmError(n, "dsm_launch_kernel_names")
+        d["kernels"] = buf.raw[:n].decode()
+        return d
 
 
 # -- host-only boundary helpers ------------------------------------------------------------

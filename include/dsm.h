@@ -35,7 +35,9 @@
 extern "C" {
 #endif
 
-#define DSM_ABI_VERSION 3   /* 3: dsm_launch_info grew resume_form / budget_rounds / ff_picked */
+#define DSM_ABI_VERSION 4   /* 3: dsm_launch_info grew resume_form / budget_rounds / ff_picked;
+                             4: dsm_counters grew to DSM_NCOUNTERS (ser_macro_steps), dsm_launch_info
+                                names the kernels that ran (dsm_launch_kernel_names) */
 
 #define DSM_MAX_NP 8             /* bitVector is one byte (README.md:51)                  */
 #define DSM_CACHE_SIZE 4         /* CACHE_SIZE      assignment.c:10                        */
@@ -134,7 +136,8 @@ typedef struct dsm_node_state {
     uint16_t issued;                   /* instructions issued (instructionIdx + 1)          */
 } dsm_node_state;
 
-/* aggregate counters (all sums except max_rounds); 32 x uint64 */
+/* aggregate counters (all sums except max_rounds); DSM_NCOUNTERS x uint64 */
+#define DSM_NCOUNTERS 40
 typedef struct dsm_counters {
     uint64_t msgs_by_type[DSM_NTYPES];   /* only with DSM_F_TYPE_COUNTS (else zero) */
     uint64_t msgs;
@@ -148,12 +151,14 @@ typedef struct dsm_counters {
     uint64_t overflow_reruns;  /* systems re-run with the 256-deep inbox */
     uint64_t wave_rounds;      /* lock-step loop iterations summed over waves (cost model) */
     uint64_t resumed;          /* systems the two-pass schedule suspended and resumed      */
-    uint64_t ff_passes;        /* multi-round steps that advanced a system: hit-run fast-
-                                * forward steps (lock-step kernels) and lone-node transaction
-                                * steps (serial resume pass, dsm_serial.h ser_macro)         */
+    uint64_t ff_passes;        /* hit-run fast-forward steps that advanced a system (the
+                                * lock-step kernels' step (0); 0 when no fast-forward ran)  */
     uint64_t ff_steps;         /* fast-forward steps per wave (cost model)                  */
     uint64_t ff_sample_instrs; /* DSM_FF_AUTO: instructions of the sampled traces           */
     uint64_t ff_sample_runs;   /* ... of them ending a run of 8 hits (a private 4-line model) */
+    uint64_t ser_macro_steps;  /* ABI 4: lone-node whole-transaction steps of the serial resume
+                                * pass (dsm_serial.h ser_macro)                              */
+    uint64_t reserved[7];      /* zero                                                       */
 } dsm_counters;
 
 typedef struct dsm_ctx dsm_ctx;
@@ -181,10 +186,23 @@ typedef struct dsm_launch_info {
                             * 1 << budget_log2, or the fast-forward budget (448) when the
                             * scan picked the hit-run fast-forward                           */
     int ff_picked;         /* 1 when the hit-run fast-forward kernel carried the run        */
+    /* ABI 4: the kernels that did the work (the pair's picked halves), for measurement
+     * labels: sim_kernel<np, ring_cap, block_threads / 64, gen, MODE, occ> */
+    int np;
+    int gen;               /* 1: the fused generator (dsm_run_generated*)                   */
+    int occ;               /* the fast kernel's waves-per-EU bound (template OCC)            */
+    int budget_mode;       /* MODE of the sim_kernel of the budget (or only) pass            */
+    int resume_mode;       /* MODE of the lock-step resume sim_kernel; -1: ser_kernel or none */
+    int ser_cap;           /* the serial resume ran ser_kernel<np, true> (inbox limit < 256) */
 } dsm_launch_info;
 
 enum { DSM_RESUME_NONE = 0, DSM_RESUME_LOCKSTEP = 1, DSM_RESUME_SERIAL = 2,
        DSM_RESUME_FASTFORWARD = 3 };
+
+/* "budget=<kernel> resume=<kernel>" (or "run=<kernel>" for one pass) of a launch info, e.g.
+ * "budget=sim_kernel<8, 12, 4, false, 48, 5> resume=ser_kernel<8, false>"; returns the
+ * length, or DSM_E_INVAL if cap is too small (host only). */
+int dsm_launch_kernel_names(const dsm_launch_info *info, char *buf, size_t cap);
 
 /* ---- library ---------------------------------------------------------------------- */
 int dsm_abi_version(void);

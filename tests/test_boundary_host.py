@@ -48,16 +48,63 @@ def _struct_fields(name):
 
 
 def test_launch_info_binding_matches_header():
-    """pydsm's ctypes mirror of dsm_launch_info (ABI 3) has the header's fields in order,
+    """pydsm's ctypes mirror of dsm_launch_info (ABI 4) has the header's fields in order,
     all of them int, so the library never writes past the caller's struct."""
     assert [f for f, _ in pydsm.LaunchInfo._fields_] == _struct_fields("dsm_launch_info")
     assert ctypes.sizeof(pydsm.LaunchInfo) == 4 * len(_struct_fields("dsm_launch_info"))
     assert set(pydsm.RESUME_FORMS) == {0, 1, 2, 3}
 
 
+def test_counter_binding_matches_header():
+    """dsm_counters (ABI 4: DSM_NCOUNTERS slots) and pydsm.COUNTER_FIELDS agree slot by slot;
+    ff_passes (hit-run fast-forward steps) and ser_macro_steps (the serial pass's lone-node
+    transaction steps) are separate slots."""
+    txt = open(os.path.join(REPO, "include", "dsm.h")).read()
+    n = int(re.search(r"#define DSM_NCOUNTERS (\d+)", txt).group(1))
+    assert n == pydsm.NCOUNTERS == len(pydsm.COUNTER_FIELDS)
+    body = re.sub(r"/\*.*?\*/", "", re.search(r"typedef struct dsm_counters \{(.*?)\} dsm_counters;",
+                                               txt, flags=re.S).group(1), flags=re.S)
+    slots = []
+    for name, arr in re.findall(r"uint64_t (\w+)(?:\[(\w+)\])?;", body):
+        k = 13 if arr == "DSM_NTYPES" else (int(arr) if arr else 1)
+        slots += [name] * k
+    assert len(slots) == n
+    for i, f in enumerate(pydsm.COUNTER_FIELDS):
+        want = {"msgs_by_type": "msgs_", "by_status": "status_", "reserved": "reserved_"}.get(slots[i], slots[i])
+        assert f.startswith(want), (i, f, slots[i])
+    assert pydsm.COUNTER_FIELDS[pydsm.MAX_SLOT] == "max_rounds"
+
+
+def _li(**kw):
+    li = pydsm.LaunchInfo()
+    base = dict(np=8, ring_cap=12, block_threads=256, gen=0, occ=5, budget_mode=48, resume_mode=-1,
+                ser_cap=0, resume_form=2)
+    for k, v in dict(base, **kw).items():
+        setattr(li, k, v)
+    return li
+
+
+@pytest.mark.parametrize("kw,want", [
+    ({}, "budget=sim_kernel<8, 12, 4, false, 48, 5> resume=ser_kernel<8, false>"),
+    (dict(ser_cap=1, np=4, budget_mode=8, resume_form=2),
+     "budget=sim_kernel<4, 12, 4, false, 8, 5> resume=ser_kernel<4, true>"),
+    (dict(budget_mode=16, resume_mode=0, resume_form=3),
+     "budget=sim_kernel<8, 12, 4, false, 16, 5> resume=sim_kernel<8, 12, 4, false, 0, 5>"),
+    (dict(budget_mode=0, gen=1, resume_form=0, ring_cap=4), "run=sim_kernel<8, 4, 4, true, 0, 5>"),
+    (dict(budget_mode=-1, resume_form=0), "none"),
+])
+def test_launch_kernel_names(kw, want):
+    """dsm_launch_kernel_names (host only): the measurement label of the kernels that ran."""
+    L = pydsm.lib()
+    buf = ctypes.create_string_buffer(256)
+    n = L.dsm_launch_kernel_names(ctypes.byref(_li(**kw)), buf, 256)
+    assert buf.raw[:n].decode() == want
+    assert L.dsm_launch_kernel_names(ctypes.byref(_li(**kw)), buf, len(want)) == pydsm.E_INVAL   # no room for the NUL
+
+
 def test_abi_version_and_errors():
     L = pydsm.lib()
-    assert L.dsm_abi_version() == 3
+    assert L.dsm_abi_version() == 4
     assert pydsm.strerror(0) == "ok"
     for code in range(-7, 0):
         assert pydsm.strerror(code) != "unknown error"

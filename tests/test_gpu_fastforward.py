@@ -148,9 +148,9 @@ def test_fast_forward_modes_agree(dsm, orc, dist):
             out[m] = eng.run_packed(tr, cn)
             _cmp(out[m][0], ores)
     off, on, auto = out[dsm.FF_OFF][1], out[dsm.FF_ON][1], out[dsm.FF_AUTO][1]
-    # off: no fast-forward step ran (ff_passes may count the serial pass's lone-node
-    # transaction steps, dsm_serial.h ser_macro: multi-round steps too)
-    assert off["ff_steps"] == 0 and off["ff_sample_instrs"] == 0
+    # off: no fast-forward step ran (the serial pass's lone-node transaction steps,
+    # dsm_serial.h ser_macro, are counted apart in ser_macro_steps)
+    assert off["ff_steps"] == 0 and off["ff_passes"] == 0 and off["ff_sample_instrs"] == 0
     assert on["ff_sample_instrs"] == 0
     assert auto["ff_sample_instrs"] == min(n, 4096) * 8 * 256
     picked = auto["ff_sample_runs"] * 16 >= auto["ff_sample_instrs"] and auto["ff_sample_runs"] > 0
@@ -173,9 +173,12 @@ def test_one_pass_pair_reports_the_kernel_that_ran(dsm, orc, dist, picked):
         info = eng.launch_info()
         assert info["ff_picked"] == picked and info["resume_form"] == 0, info
         assert info["budget_log2"] == 0 and info["budget_rounds"] == 0, info
+        # the label names the picked half of the pair: MODE 0 (fast-forward) or M_NOFF (16)
+        assert info["kernels"] == f"run=sim_kernel<8, 12, 4, false, {0 if picked else 16}, 5>", info
         eng.run_packed(tr[:0], cn[:0])
         info = eng.launch_info()
         assert info["grid_blocks"] == 0 and info["ff_picked"] == 0 and info["resume_form"] == 0, info
+        assert info["kernels"] == "none", info
     ores = orc.run_packed(8, tr, cn, nthreads=16)[0]
     _cmp(res, ores)
 

@@ -9,6 +9,8 @@ import pytest
 from conftest import (GOLD, TESTS, golden_aggregate, golden_dump, golden_ensemble, golden_ensemble_recs,
                       golden_records, inputs_dir, res_to_u64)
 
+import pydsm  # noqa: E402  (numpy + ctypes only; the library loads lazily)
+
 pytestmark = pytest.mark.gpu
 
 
@@ -157,7 +159,7 @@ def test_device_entry_points_and_accumulation(dsm, orc):
         tr = torch.empty((n, 8, 4096), dtype=torch.int16, device="cuda")
         cn = torch.empty((n, 8), dtype=torch.int32, device="cuda")
         out = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-        cnt = torch.zeros(32, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device="cuda")
         eng.generate_device("evict", 3, 4096, 1000, n, tr.data_ptr(), cn.data_ptr(), st)
         eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
         eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
@@ -219,7 +221,7 @@ def test_full_size_1m_random(dsm, orc):
         tr = torch.empty((n, 8, 4096), dtype=torch.int16, device="cuda")
         cn = torch.empty((n, 8), dtype=torch.int32, device="cuda")
         out = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-        cnt = torch.zeros(32, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device="cuda")
         eng.generate_device("uniform", 1, 4096, 0, n, tr.data_ptr(), cn.data_ptr(), st)
         eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
         torch.cuda.synchronize()
@@ -256,7 +258,7 @@ def test_full_size_c4_c5(dsm, orc, dist, n):
         tr = torch.empty((n, 8, 4096), dtype=torch.int16, device="cuda")
         cn = torch.empty((n, 8), dtype=torch.int32, device="cuda")
         out = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-        cnt = torch.zeros(32, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device="cuda")
         eng.generate_device(dist, 1, 4096, 0, n, tr.data_ptr(), cn.data_ptr(), st)
         eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
         torch.cuda.synchronize()

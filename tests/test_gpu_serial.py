@@ -14,6 +14,8 @@ import pytest
 
 from conftest import res_to_u64
 
+import pydsm  # noqa: E402  (numpy + ctypes only; the library loads lazily)
+
 pytestmark = pytest.mark.gpu
 
 
@@ -148,7 +150,7 @@ def test_serial_assert_home_beyond_np(dsm, orc, monkeypatch):
         dtr = torch.from_numpy(tr.view(np.int16)).cuda()
         dcn = torch.from_numpy(cn.view(np.int32)).cuda()
         out = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-        c = torch.zeros(32, dtype=torch.int64, device="cuda")
+        c = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device="cuda")
         eng.run_packed_device(dtr.data_ptr(), dcn.data_ptr(), n, out.data_ptr(), c.data_ptr(), st)
         torch.cuda.synchronize()
         res = out.cpu().numpy().view(dsm.RESULT_DTYPE).reshape(-1)

@@ -12,6 +12,8 @@ import pytest
 
 from conftest import res_to_u64
 
+import pydsm  # noqa: E402  (numpy + ctypes only; the library loads lazily)
+
 pytestmark = pytest.mark.gpu
 
 
@@ -25,10 +27,10 @@ def dsm():
 
 def _reduce(vecs):
     """bench.reduce_counters on host vectors."""
-    tot = np.zeros(32, dtype=np.uint64)
+    tot = np.zeros(pydsm.NCOUNTERS, dtype=np.uint64)
     for v in vecs:
         tot += v
-    tot[24] = max(int(v[24]) for v in vecs)
+    tot[pydsm.MAX_SLOT] = max(int(v[pydsm.MAX_SLOT]) for v in vecs)
     return tot
 
 
@@ -41,7 +43,7 @@ def test_four_shards_equal_one_shot(dsm, dist, packed):
     with dsm.Engine(8, 4096) as eng:
         def run(first, cnt_sys):
             out = torch.zeros((cnt_sys, 4), dtype=torch.int64, device="cuda")
-            cnt = torch.zeros(32, dtype=torch.int64, device="cuda")
+            cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device="cuda")
             if packed:
                 tr = torch.empty((cnt_sys, 8, 4096), dtype=torch.int16, device="cuda")
                 cn = torch.empty((cnt_sys, 8), dtype=torch.int32, device="cuda")
@@ -79,7 +81,7 @@ def test_run_packed_device_does_not_wait(dsm):
         tr = torch.empty((n, 8, 4096), dtype=torch.int16, device="cuda")
         cn = torch.empty((n, 8), dtype=torch.int32, device="cuda")
         out = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-        cnt = torch.zeros(32, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device="cuda")
         eng.generate_device("uniform", 1, 4096, 0, n, tr.data_ptr(), cn.data_ptr(), st)
         eng.run_packed_device(tr.data_ptr(), cn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
         torch.cuda.synchronize()

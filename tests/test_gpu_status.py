@@ -18,6 +18,8 @@ import pytest
 
 from conftest import ORACLE, res_to_u64
 
+import pydsm  # noqa: E402  (numpy + ctypes only; the library loads lazily)
+
 pytestmark = pytest.mark.gpu
 
 
@@ -48,7 +50,7 @@ def _run_device(dsm, eng, tr, cn):
     dtr = torch.from_numpy(tr.view(np.int16)).cuda()
     dcn = torch.from_numpy(cn.view(np.int32)).cuda()
     out = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-    cnt = torch.zeros(32, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device="cuda")
     eng.run_packed_device(dtr.data_ptr(), dcn.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), st)
     torch.cuda.synchronize()
     return (out.cpu().numpy().view(dsm.RESULT_DTYPE).reshape(-1),

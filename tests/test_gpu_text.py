@@ -10,6 +10,8 @@ import pytest
 
 from conftest import GOLD, TESTS, golden_dump, inputs_dir
 
+import pydsm  # noqa: E402  (numpy + ctypes only; the library loads lazily)
+
 pytestmark = pytest.mark.gpu
 
 
@@ -111,7 +113,7 @@ def test_gpu_format_full_size_final_view(dsm, torch):
     st = torch.cuda.current_stream().cuda_stream
     with dsm.Engine(8, 4096, snapshots=True) as eng:
         out = torch.empty((n_sys, 4), dtype=torch.int64, device=dev)
-        cnt = torch.zeros(32, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device=dev)
         eng.run_generated_device("uniform", 1, 4096, 0, n_sys, out.data_ptr(), cnt.data_ptr(), st)
         d_txt = torch.empty(n_sys * 8 * dsm.DUMP_SLOT, dtype=torch.uint8, device=dev)
         d_len = torch.zeros(n_sys * 8, dtype=torch.int32, device=dev)

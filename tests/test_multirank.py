@@ -15,12 +15,14 @@ import torch.multiprocessing as mp
 
 from conftest import REPO
 
+import pydsm  # noqa: E402  (numpy + ctypes only; the library loads lazily)
+
 N_PER_RANK = 96
 
 
 def counters_from_results(res):
     """dsm_counters layout (include/dsm.h) from per-system results."""
-    c = np.zeros(32, dtype=np.uint64)
+    c = np.zeros(pydsm.NCOUNTERS, dtype=np.uint64)
     c[13] = res["msgs"].sum(dtype=np.uint64)
     c[14] = res["instrs"].sum(dtype=np.uint64)
     c[15] = res["rounds"].sum(dtype=np.uint64)

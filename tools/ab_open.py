@@ -29,7 +29,7 @@ st = torch.cuda.current_stream(dev).cuda_stream
 tr = torch.empty((n, 8, 4096), dtype=torch.int16, device=dev)
 cn = torch.empty((n, 8), dtype=torch.int32, device=dev)
 out = torch.empty((n, 4), dtype=torch.int64, device=dev)
-cnt = torch.zeros(32, dtype=torch.int64, device=dev)
+cnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device=dev)
 with pydsm.Engine(8, 4096) as g:
     g.generate_device(dist, 1, 4096, 0, n, tr.data_ptr(), cn.data_ptr(), st)
 res = {v: [] for v in variants}

@@ -27,8 +27,8 @@ torch.cuda.synchronize()
 streams = [torch.cuda.Stream(dev) for _ in range(parts)]
 engs = [pydsm.Engine(8, 4096) for _ in range(parts)]
 one = pydsm.Engine(8, 4096)
-cnts = [torch.zeros(32, dtype=torch.int64, device=dev) for _ in range(parts)]
-c1 = torch.zeros(32, dtype=torch.int64, device=dev)
+cnts = [torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device=dev) for _ in range(parts)]
+c1 = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device=dev)
 cut = [n * i // parts for i in range(parts + 1)]
 
 
