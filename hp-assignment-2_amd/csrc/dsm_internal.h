@@ -78,6 +78,8 @@ struct dsm_ctx {
     size_t parse_cap;
     uint64_t *d_parse_off;
     size_t parse_off_cap;
+    uint32_t *d_parse_list;          /* parse_kernel: [0] files for the EXACT pass, then ids  */
+    size_t parse_list_cap;
 };
 
 #define HIPCK(x) do { if ((x) != hipSuccess) return DSM_E_DEVICE; } while (0)

@@ -283,10 +283,46 @@ DEVI uint32_t parse_fast_swar(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t li
     const uint32_t lok = rd ? (uint32_t)(lim >= 8u) : (wr & wv & (uint32_t)(lim >= 9u + p));
     return c1ok & h2ok & lok;
 }
-#ifndef PARSE_SWAR
-#define PARSE_SWAR 1        /* parse_fast_swar in the chunk loop: 8.96-8.98 vs 9.31-9.35 ms (parse_fast) */
+/* v_dot4_u32_u8 (a's four bytes times b's, summed, plus c); host form for the decoder tests */
+DEVI uint32_t udot4(uint32_t a, uint32_t b, uint32_t c) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_udot4(a, b, c, false);
+#else
+    for (int i = 0; i < 32; i += 8) c += ((a >> i) & 0xFFu) * ((b >> i) & 0xFFu);
+    return c;
 #endif
-#if PARSE_SWAR
+}
+/* parse_fast_swar with nothing the compiler turns into a branch: the WR value is one
+ * v_dot4_u32_u8 of its digits (aligned to bytes 0-2) with (100, 10, 1), computed for every
+ * chunk (a lane's RD and WR chunks are one data flow, not two exec-masked paths), and the
+ * address's low digit is (b & 15) + 9 * bit 6 of b once b is known to be a hex digit. */
+DEVI uint32_t parse_fast_v3(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t lim, uint32_t *pk) {
+    const uint32_t rd = (uint32_t)(c0 == 0x30204452u), wr = (uint32_t)(c0 == 0x30205257u);
+    const uint32_t want = 0x0A003078u ^ ((0u - wr) & 0x2A000000u);  /* b7 '\n' (RD) or ' ' (WR) */
+    const uint32_t c1ok = (uint32_t)(((c1 ^ want) & 0xFF00F8FFu) == 0u);
+    const uint32_t b6 = __builtin_amdgcn_ubfe(c1, 16, 8);
+    const uint32_t h2ok = (uint32_t)(b6 - 0x30u < 10u) | (uint32_t)((b6 | 0x20u) - 0x61u < 6u);
+    const uint32_t lo4 = (b6 & 15u) + 9u * ((b6 >> 6) & 1u);
+    const uint32_t a = (__builtin_amdgcn_ubfe(c1, 8, 3) << 4) | lo4;
+    const uint32_t y = c2 ^ 0x30303030u;                            /* digits -> 0..9 */
+    const uint32_t nd = (((y & 0x7F7F7F7Fu) + 0x76767676u) | y) & 0x80808080u;  /* non-digit */
+    const uint32_t z = c2 ^ 0x0A0A0A0Au;
+    const uint32_t nlb = ~((((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z)) & 0x80808080u; /* newline */
+    const uint32_t fb = nd & (0u - nd);                             /* first non-digit byte's bit */
+    const uint32_t wv = (uint32_t)((fb & nlb) != 0u) & (uint32_t)(fb != 0x80u);
+    const uint32_t p = (uint32_t)__builtin_ctz(nd | 0x80000000u) >> 3;   /* digits before it */
+    const uint32_t v = udot4(y << (24u - 8u * p), 0x00010A64u, 0u);
+    *pk = (wr << 15) | (a << 8) | ((0u - wr) & v & 0xFFu);
+    const uint32_t need = wr ? 9u + p : 8u;
+    const uint32_t lok = (uint32_t)(lim >= need) & (rd | (wr & wv));
+    return c1ok & h2ok & lok;
+}
+#ifndef PARSE_SWAR
+#define PARSE_SWAR 2        /* 2: parse_fast_v3; 1: parse_fast_swar (8.96-8.98 vs 9.31-9.35 ms, parse_fast) */
+#endif
+#if PARSE_SWAR == 2
+#define PARSE_FAST parse_fast_v3
+#elif PARSE_SWAR
 #define PARSE_FAST parse_fast_swar
 #else
 #define PARSE_FAST parse_fast
@@ -297,26 +333,39 @@ DEVI uint32_t lowmask(uint32_t n) { return n >= 32u ? 0xFFFFFFFFu : (1u << n) - 
 
 /* One file per wave; windows of 64 x BPL bytes, double-buffered in registers (the next
  * window's loads are in flight while this one is scanned), staged in LDS for the chunk
- * reads. */
+ * reads.
+ *
+ * Two builds of the same kernel.  FAST (the first pass over every file) has no cold path: a
+ * window with a line that needs chunks every 19 bytes, or a chunk the canonical-line decoder
+ * declines, abandons the whole file, which goes on a device list; the EXACT build (the second
+ * pass) reads only the listed files, with the per-byte chunking of long lines and the exact
+ * scanner of dsm_parse.h.  Generated and shipped core files never reach the second pass.
+ * Splitting them (round 5) took the cold paths' code and registers out of the hot kernel:
+ * 77 VGPRs with no spills at 6 waves per SIMD instead of 80 with 8-10 spilled, 7.4 vs 8.4 ms
+ * on the bench's 21-GB text. */
 #ifndef PARSE_OCC
 #define PARSE_OCC 6
 #endif
 #ifndef PARSE_TRANSPOSE
 #define PARSE_TRANSPOSE 1   /* newline mask by one 4 x 8 bit transpose: 8.23-8.36 vs 8.91-8.96 ms */
 #endif
-#ifndef PARSE_UNROLL
-#define PARSE_UNROLL 0      /* the chunk loop's first 4 chunks per lane in two fixed rounds */
+#ifndef PARSE_PROBE
+#define PARSE_PROBE 0       /* timing probes of the FAST pass (results invalid): 1 no decode, 2 decode
+                               without the store, 3 decode with the chunk words from registers */
 #endif
-template <uint32_t BPL>
-__global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PARSE_OCC))) parse_kernel(const uint8_t *text, const uint64_t *off,
-                                                      uint64_t n_files, uint32_t cap,
-                                                      uint32_t stride, int np, uint16_t *traces,
-                                                      uint32_t *counts, int32_t *status) {
+template <uint32_t BPL, bool FAST>
+__global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PARSE_OCC)))
+parse_kernel(const uint8_t *text, const uint64_t *off, uint64_t n_files, uint32_t cap,
+             uint32_t stride, int np, uint16_t *traces, uint32_t *counts, int32_t *status,
+             uint32_t *flist, uint32_t *fcount) {
     constexpr uint32_t K = BPL / 16, WIN = 64 * BPL;
     __shared__ __attribute__((aligned(16))) uint8_t s_txt[PW][WIN + PHALO + 16];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint8_t *const st = s_txt[wv];
-    for (uint64_t f = (uint64_t)blockIdx.x * PW + wv; f < n_files; f += (uint64_t)gridDim.x * PW) {
+    /* FAST: every file; EXACT: the files FAST abandoned (flist[0 .. *fcount)) */
+    const uint64_t nf = FAST ? n_files : (uint64_t)*fcount;
+    for (uint64_t k = (uint64_t)blockIdx.x * PW + wv; k < nf; k += (uint64_t)gridDim.x * PW) {
+        const uint64_t f = FAST ? k : (uint64_t)flist[k];
         const uint64_t b0 = off[f], b1 = off[f + 1];
         uint16_t *const out = traces + f * stride;
         const uint64_t wbeg = b0 & ~15ull;
@@ -337,9 +386,11 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
         uint32_t ls_rel = s0;         /* start of the line open at the window start          */
         uint32_t idx0 = 0;            /* chunks before the window                           */
         uint32_t err = 0xFFFFFFFFu;   /* first failing chunk: index * 8 + error class        */
+        bool bad = false;             /* FAST: the file needs the EXACT pass                  */
         uint4 va[K], vb[K], ha, hb;
         uint64_t wa = wbeg;
         bool more = wbeg < b1;
+        uint32_t psum = 0;            /* PARSE_PROBE 2: keeps the decode live */
         if (more) load(wa, va, ha);
         auto window = [&](uint64_t wa, const uint4 (&v)[K], const uint4 &h) {
             /* (1) stage [wa, wa + WIN + PHALO) */
@@ -397,7 +448,11 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
             const uint32_t t1 = r & (r >> 1), t2 = t1 & (t1 >> 2), t4 = t2 & (t2 >> 4), t8 = t4 & (t4 >> 8);
             const bool run19 = BPL > DP_CHUNK && (t8 & (t1 >> 16) & (r >> 18)) != 0u;
             /* (lanes past the file's end have no bytes: fm == 0 keeps them out) */
-            if (fm != 0u && ((lo == 0 && din + (fnl < BPL - 1u ? fnl : BPL - 1u) >= DP_CHUNK) || run19)) {   /* long line */
+            const bool longl = fm != 0u && ((lo == 0 && din + (fnl < BPL - 1u ? fnl : BPL - 1u) >= DP_CHUNK) || run19);
+            if (FAST) {
+                bad = __ballot(longl) != 0;              /* a long line: the EXACT pass */
+                if (bad) return;
+            } else if (longl) {
                 uint32_t d = din % DP_CHUNK;
                 cs = 0;
                 for (uint32_t j = 0; j < BPL; ++j) {
@@ -413,68 +468,40 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
             const uint32_t T = __builtin_amdgcn_readlane(isum, 63);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             /* (6) each lane parses the chunks that start in its bytes, one per round, from
-             * LDS (no compaction pass: about as many rounds, ~3 of the ~4 lines per lane),
-             * 2-byte stores at their instruction index */
+             * LDS, 2-byte stores at their instruction index */
             const uint32_t tmax = cap - idx0 < T ? cap - idx0 : T;
             const uint32_t rem = e0 - wr0;                       /* file bytes from wa on */
             /* the fast path only, in a tight loop; the chunks it declines (any other shape,
-             * an address whose home is >= np) are marked in `slow` and scanned exactly after
-             * the loop -- inside it, the rare branch's code and registers slowed every round */
+             * an address whose home is >= np) are marked in `slow` and, in the EXACT pass,
+             * scanned exactly after the loop */
             uint32_t mcs = cs, t = isum - nc, slow = 0;
-#if PARSE_UNROLL
-            /* a canonical line is >= 8 bytes, so at most 4 chunks start in a lane's 32 bytes:
-             * two fixed rounds of two independent chunks (their LDS reads issued together, no
-             * ballot or branch between them), then the rest, if any, in the loop below */
-            auto chunk_at = [&](uint32_t b, uint32_t &c0, uint32_t &c1, uint32_t &c2) {
-                const uint32_t o = BPL * lane + b;
-                const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
-                const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
-                c0 = __builtin_amdgcn_alignbyte(d1, d0, o & 3u);
-                c1 = __builtin_amdgcn_alignbyte(d2, d1, o & 3u);
-                c2 = __builtin_amdgcn_alignbyte(d3, d2, o & 3u);
-            };
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                const bool ea = (mcs != 0u) & (t < tmax);
-                const uint32_t ba = (uint32_t)__builtin_ctz(mcs | 0x80000000u);
-                mcs &= mcs - 1u;
-                const bool eb = (mcs != 0u) & (t + 1u < tmax);
-                const uint32_t bb = (uint32_t)__builtin_ctz(mcs | 0x80000000u);
-                mcs &= mcs - 1u;
-                uint32_t a0, a1, a2, b0_, b1_, b2_;
-                chunk_at(ba, a0, a1, a2);
-                chunk_at(bb, b0_, b1_, b2_);
-                const uint32_t oa = BPL * lane + ba, ob = BPL * lane + bb;
-                const uint32_t la = rem - oa < DP_CHUNK ? rem - oa : DP_CHUNK;
-                const uint32_t lb = rem - ob < DP_CHUNK ? rem - ob : DP_CHUNK;
-                uint32_t pa = 0, pb = 0;
-                const bool oka = PARSE_FAST(a0, a1, a2, la, &pa) & (((pa >> 12) & 7u) < (uint32_t)np);
-                const bool okb = PARSE_FAST(b0_, b1_, b2_, lb, &pb) & (((pb >> 12) & 7u) < (uint32_t)np);
-                if (ea & oka) out[idx0 + t] = (uint16_t)pa;
-                if (eb & okb) out[idx0 + t + 1u] = (uint16_t)pb;
-                slow |= (ea & !oka) ? 1u << ba : 0u;
-                slow |= (eb & !okb) ? 1u << bb : 0u;
-                t += 2u;
-            }
-#endif
+            if (FAST && PARSE_PROBE == 1) mcs = 0;
             while (__ballot((mcs != 0u) & (t < tmax))) {
                 if ((mcs != 0u) & (t < tmax)) {
                     const uint32_t b = (uint32_t)__builtin_ctz(mcs), o = BPL * lane + b;
                     const uint32_t lim = rem - o < DP_CHUNK ? rem - o : DP_CHUNK;
-                    const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
-                    const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
+                    uint32_t d0, d1, d2, d3;
+                    if (FAST && PARSE_PROBE == 3) {
+                        d0 = v[0].x ^ o; d1 = v[0].y ^ t; d2 = v[0].z; d3 = v[0].w;
+                    } else {
+                        const uint32_t *wd = reinterpret_cast<const uint32_t *>(st + (o & ~3u));
+                        d0 = wd[0]; d1 = wd[1]; d2 = wd[2]; d3 = wd[3];
+                    }
                     const uint32_t c0 = __builtin_amdgcn_alignbyte(d1, d0, o & 3u);
                     const uint32_t c1 = __builtin_amdgcn_alignbyte(d2, d1, o & 3u);
                     const uint32_t c2 = __builtin_amdgcn_alignbyte(d3, d2, o & 3u);
                     uint32_t pk = 0;
                     const bool ok = PARSE_FAST(c0, c1, c2, lim, &pk) & (((pk >> 12) & 7u) < (uint32_t)np);
-                    if (ok) out[idx0 + t] = (uint16_t)pk;
+                    if (FAST && PARSE_PROBE == 2) psum += ok ? pk : 1u;
+                    else if (ok) out[idx0 + t] = (uint16_t)pk;
                     slow |= ok ? 0u : 1u << b;
                 }
                 mcs &= mcs - 1u;
                 ++t;
             }
-            if (__ballot(slow != 0u)) {
+            if (FAST) {
+                if (PARSE_PROBE < 2) bad = __ballot(slow != 0u) != 0;   /* declined: EXACT pass */
+            } else if (__ballot(slow != 0u)) {
                 for (uint32_t m = slow; m; m &= m - 1u) {
                     const uint32_t b = (uint32_t)__builtin_ctz(m), o = BPL * lane + b;
                     const uint32_t ti = isum - nc + (uint32_t)__builtin_popcount(cs & lowmask(b));
@@ -489,8 +516,8 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
                         err = e < err ? e : err;
                     }
                 }
+                if (__ballot(err != 0xFFFFFFFFu)) err = wave_min(err);
             }
-            if (__ballot(err != 0xFFFFFFFFu)) err = wave_min(err);
             idx0 += T;
             ls_rel = umax(ls_rel, __builtin_amdgcn_readlane(incl, 63));
         };
@@ -500,24 +527,29 @@ __global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PA
             const uint64_t wn = wa + WIN;
             load(wn, vb, hb);
             window(wa, va, ha);
-            more = wn < b1 && idx0 < cap && err == 0xFFFFFFFFu;
+            more = wn < b1 && idx0 < cap && err == 0xFFFFFFFFu && !bad;
             if (!more) break;
             wa = wn;
             const uint64_t wn2 = wa + WIN;
             load(wn2, va, ha);
             window(wa, vb, hb);
-            more = wn2 < b1 && idx0 < cap && err == 0xFFFFFFFFu;
+            more = wn2 < b1 && idx0 < cap && err == 0xFFFFFFFFu && !bad;
             wa = wn2;
         }
+        if (FAST && PARSE_PROBE == 2 && psum == 0x9E3779B9u) out[lane] = 0;
         if (lane == 0) {
-            uint32_t n = idx0 < cap ? idx0 : cap;
-            int32_t sc = DSM_OK;
-            if (err != 0xFFFFFFFFu && (err >> 3) < n) {
-                n = err >> 3;
-                sc = (err & 7u) == 1u ? DSM_E_FORMAT : DSM_E_RANGE;
+            if (FAST && bad) {
+                flist[atomicAdd(fcount, 1u)] = (uint32_t)f;     /* to the EXACT pass */
+            } else {
+                uint32_t n = idx0 < cap ? idx0 : cap;
+                int32_t sc = DSM_OK;
+                if (err != 0xFFFFFFFFu && (err >> 3) < n) {
+                    n = err >> 3;
+                    sc = (err & 7u) == 1u ? DSM_E_FORMAT : DSM_E_RANGE;
+                }
+                counts[f] = n;
+                if (status) status[f] = sc;
             }
-            counts[f] = n;
-            if (status) status[f] = sc;
         }
     }
 }
@@ -600,7 +632,8 @@ __global__ void __launch_bounds__(256) textgen_kernel(uint64_t seed, int dist, u
 /* ====================================================================================== */
 
 void dsm_text_release(dsm_ctx *c) {
-    void *ptrs[] = {c->d_dump_tpl, c->d_text_tmp, c->d_len_tmp, c->d_parse_buf, c->d_parse_off};
+    void *ptrs[] = {c->d_dump_tpl, c->d_text_tmp, c->d_len_tmp, c->d_parse_buf, c->d_parse_off,
+                    c->d_parse_list};
     for (void *p : ptrs) if (p) (void)hipFree(p);
 }
 
@@ -724,27 +757,42 @@ extern "C" int dsm_parse_traces_device(dsm_ctx *c, const char *d_text, const uin
     if (!c || cap > c->cfg.max_instr) return DSM_E_INVAL;
     if (n_files && (!d_text || !d_offsets || !d_traces || !d_counts)) return DSM_E_INVAL;
     if (n_files == 0) return DSM_OK;
+    if (n_files > 0xFFFFFFFFull) return DSM_E_INVAL;
     HIPCK(hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    /* the EXACT pass's file list: [0] = count, then file ids */
+    int rc = dsm_ensure(&c->d_parse_list, &c->parse_list_cap, (size_t)n_files + 1);
+    if (rc) return rc;
+    HIPCK(hipMemsetAsync(c->d_parse_list, 0, sizeof(uint32_t), st));
     /* DSM_PARSE_BPL=16|32 (read at dsm_open): bytes per lane per window (1 or 2 KB
      * windows), for A/B runs */
     const bool b32 = c->parse_bpl != 16;
-    const void *fn = b32 ? (const void *)parse_kernel<32> : (const void *)parse_kernel<16>;
+    const void *fast = b32 ? (const void *)parse_kernel<32, true> : (const void *)parse_kernel<16, true>;
     /* one resident round of workgroups: a grid-stride loop over files with a second, partial
      * round of workgroups would leave most of the chip idle at the end */
     int per_cu = 0;
-    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * PW, 0));
+    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fast, 64 * PW, 0));
     if (per_cu < 1) per_cu = 1;
     uint64_t blocks = (n_files + PW - 1) / PW;
     const uint64_t lim = (uint64_t)c->cus * per_cu;
     if (blocks > lim) blocks = lim;
-    if (b32)
-        hipLaunchKernelGGL(parse_kernel<32>, dim3((unsigned)blocks), dim3(64 * PW), 0, (hipStream_t)stream,
-                           (const uint8_t *)d_text, d_offsets, n_files, cap, c->cfg.max_instr,
-                           c->cfg.np, d_traces, d_counts, d_status);
-    else
-        hipLaunchKernelGGL(parse_kernel<16>, dim3((unsigned)blocks), dim3(64 * PW), 0, (hipStream_t)stream,
-                           (const uint8_t *)d_text, d_offsets, n_files, cap, c->cfg.max_instr,
-                           c->cfg.np, d_traces, d_counts, d_status);
+    uint32_t *fl = c->d_parse_list + 1, *fc = c->d_parse_list;
+    const uint8_t *tx = (const uint8_t *)d_text;
+    const uint32_t mi = c->cfg.max_instr;
+    const int np = c->cfg.np;
+    /* the FAST pass over every file, then the EXACT pass over the files it listed (sized on
+     * the device: its workgroups past the list's count exit at once) */
+    if (b32) {
+        hipLaunchKernelGGL((parse_kernel<32, true>), dim3((unsigned)blocks), dim3(64 * PW), 0, st,
+                           tx, d_offsets, n_files, cap, mi, np, d_traces, d_counts, d_status, fl, fc);
+        hipLaunchKernelGGL((parse_kernel<32, false>), dim3((unsigned)blocks), dim3(64 * PW), 0, st,
+                           tx, d_offsets, n_files, cap, mi, np, d_traces, d_counts, d_status, fl, fc);
+    } else {
+        hipLaunchKernelGGL((parse_kernel<16, true>), dim3((unsigned)blocks), dim3(64 * PW), 0, st,
+                           tx, d_offsets, n_files, cap, mi, np, d_traces, d_counts, d_status, fl, fc);
+        hipLaunchKernelGGL((parse_kernel<16, false>), dim3((unsigned)blocks), dim3(64 * PW), 0, st,
+                           tx, d_offsets, n_files, cap, mi, np, d_traces, d_counts, d_status, fl, fc);
+    }
     HIPCK(hipGetLastError());
     return DSM_OK;
 }

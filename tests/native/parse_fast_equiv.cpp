@@ -6,6 +6,7 @@
 #include <cstring>
 #include <random>
 #define DEVI static inline
+static inline uint32_t __builtin_amdgcn_ubfe(uint32_t w, uint32_t o, uint32_t n) { return (w >> o) & ((1u << n) - 1u); }
 #include "pf.h"   /* parse_fast .. parse_fast_swar, cut from csrc/dsm_text.hip by the test */
 static uint32_t W(const unsigned char *b, int i) { uint32_t x; memcpy(&x, b + i, 4); return x; }
 int main() {
@@ -16,7 +17,10 @@ int main() {
         uint32_t p1 = 0, p2 = 0;
         uint32_t o1 = parse_fast(W(b,0), W(b,4), W(b,8), lim, &p1);
         uint32_t o2 = parse_fast_swar(W(b,0), W(b,4), W(b,8), lim, &p2);
+        uint32_t p3 = 0;
+        uint32_t o3 = parse_fast_v3(W(b,0), W(b,4), W(b,8), lim, &p3);
         ++n; acc += o1;
+        if (o1 != o3 || (o1 && p1 != p3)) { printf("MISMATCH v3 o %u %u pk %x %x lim %u:", o1, o3, p1, p3, lim); for (int k = 0; k < 12; ++k) printf(" %02x", b[k]); printf("\n"); return false; }
         if (o1 != o2 || (o1 && p1 != p2)) { printf("MISMATCH o %u %u pk %x %x lim %u:", o1, o2, p1, p2, lim); for (int k = 0; k < 12; ++k) printf(" %02x", b[k]); printf("\n"); return false; }
         return true;
     };
