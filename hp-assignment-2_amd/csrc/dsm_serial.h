@@ -402,12 +402,17 @@ DSM_HD uint32_t ser_step(M &m, SReg &r, const T &tab, F &&fetch, R &&on_dump, ui
  * Returns false, changing nothing but the fetch cache, when the system is not in such a state
  * or the transaction would send anything else; ser_step then takes it one action at a time.
  * Not used in the CAP build (its per-node inbox counts are not kept here). */
+/* the most rounds one ser_macro call adds: the request after an eviction at the same home
+ * (3), then a forward and its flush (2).  ser_quiet_lone keeps that many plus the round after
+ * (a fan-out's INVs) below the round limit; the host model checks every call's advance
+ * against it (tests/model/serial_model.cpp). */
+constexpr uint32_t SER_MACRO_MAX_ROUNDS = 5;
 DSM_HD bool ser_quiet_lone(const SReg &r, uint32_t lim_rsh) {
     /* nothing queued or spilled, exactly one node may act and it is the only one left in the
-     * round, and the round limit is out of reach of the transaction's <= 5 rounds and the
-     * round after (a fan-out's INVs) */
+     * round, and the round limit is out of reach of the transaction's rounds and the round
+     * after */
     return (r.nz | (r.q & 0xFFF8u) | r.spl) == 0u && r.A == r.iss && r.A != 0u && (r.A & (r.A - 1u)) == 0u &&
-           ((r.rounds + 6u) >> lim_rsh) == 0u;
+           ((r.rounds + SER_MACRO_MAX_ROUNDS + 1u) >> lim_rsh) == 0u;
 }
 
 /* the lone node's own words (control, line addresses, line values) held in registers

@@ -98,8 +98,14 @@ int run(int dist, uint64_t n_sys, uint32_t lim_log2, uint32_t n_instr, uint32_t 
         do {
             /* as the kernel: a lone node's whole transaction at once when it applies */
             if (macro && cap >= 256u && dsms::ser_quiet_lone(r, lim)) {
+                const uint32_t r0 = r.rounds;
                 if (dsms::ser_macro<NP>(m, r, cc, fetch_try, on_dump, [](int) {})) {
                     ++n_macro;
+                    if (r.rounds - r0 > dsms::SER_MACRO_MAX_ROUNDS) {     /* the quiet-lone margin */
+                        fprintf(stderr, "ser_macro advanced %u rounds (> %u)\n", r.rounds - r0,
+                                dsms::SER_MACRO_MAX_ROUNDS);
+                        return 3;
+                    }
                     v = r.A ? dsms::SR_RUN : dsms::SR_DONE;     /* a dead-end forward ends it */
                     continue;
                 }

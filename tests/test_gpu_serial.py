@@ -175,9 +175,13 @@ def test_serial_small_ensembles(dsm, orc, monkeypatch, n):
     assert cnt["systems"] == n and cnt["resumed"] > 0
 
 
-@pytest.mark.parametrize("np_,dist,lone_min", [(8, "uniform", 0), (8, "evict", 0), (8, "uniform", 256),
-                                               (4, "uniform", 0)])
-def test_suspend_on_lone_is_exact(dsm, orc, monkeypatch, np_, dist, lone_min):
+@pytest.mark.parametrize("np_,dist,lone_min,ring,icap", [
+    (8, "uniform", 0, 12, 0), (8, "evict", 0, 12, 0), (8, "uniform", 256, 12, 0), (4, "uniform", 0, 12, 0),
+    # the serial-form record laid out for ring 4 (overflow-prone: re-runs compose with it) and
+    # ring 16 (the 264-word record), and read by the CAP build (an inbox limit between the
+    # ring and 256 keeps the bench mode, so the budget pass writes the serial form)
+    (8, "uniform", 0, 4, 0), (8, "uniform", 0, 16, 0), (8, "uniform", 0, 12, 64)])
+def test_suspend_on_lone_is_exact(dsm, orc, monkeypatch, np_, dist, lone_min, ring, icap):
     """The budget pass suspends quiet-lone systems (DSM_LONE, checked every 8 rounds, from
     DSM_LONE_MIN rounds on) in the serial-form record; the serial pass resumes them with its
     lone-node macro-step.  Results and records equal the oracle and a run without it, and the
@@ -189,9 +193,13 @@ def test_suspend_on_lone_is_exact(dsm, orc, monkeypatch, np_, dist, lone_min):
     for lone in ("0", "8"):
         monkeypatch.setenv("DSM_LONE", lone)
         monkeypatch.setenv("DSM_LONE_MIN", str(lone_min))
-        with dsm.Engine(np_, 4096, snapshots=True) as eng:
+        with dsm.Engine(np_, 4096, ring_cap=ring, snapshots=True) as eng:
+            if icap:
+                eng.set_inbox_limit(icap)
             res, cnt = eng.run_packed(tr, cn)
-            assert eng.launch_info()["resume_form"] == 2
+            li = eng.launch_info()
+            assert li["resume_form"] == 2 and li["ring_cap"] == ring, li
+            assert li["ser_cap"] == (1 if icap else 0), li
             for s in range(0, n, 83):
                 mask = int(ores[s]["status"]) >> 8
                 for nd in range(np_):
@@ -200,7 +208,14 @@ def test_suspend_on_lone_is_exact(dsm, orc, monkeypatch, np_, dist, lone_min):
                     if (mask >> nd) & 1:
                         assert np.array_equal(d, odump[s, nd])
         _cmp(res, ores)
-        assert cnt["msgs"] == int(ores["msgs"].sum()) and cnt["overflow_reruns"] == 0
+        assert cnt["msgs"] == int(ores["msgs"].sum())
+        if ring >= 12:
+            assert cnt["overflow_reruns"] == 0
+        # the lone-node macro-step runs only in the default (non-CAP) serial build
+        if icap:
+            assert cnt["ser_macro_steps"] == 0, cnt
+        elif lone == "8":
+            assert cnt["ser_macro_steps"] > 0, cnt
         out[lone] = cnt
     assert out["8"]["resumed"] > out["0"]["resumed"], (out["8"]["resumed"], out["0"]["resumed"])
     assert out["8"]["sum_final_hash"] == out["0"]["sum_final_hash"]
