@@ -105,6 +105,10 @@ struct SimArgsPack { SimArgs a[3]; };
 
 #define DEVI __device__ __forceinline__
 
+#ifndef TRAFFIC_PROBE
+#define TRAFFIC_PROBE 0     /* traffic attribution builds (results invalid): 1 no serial pass, 2 and
+                               no serial-form suspend records (tools/traffic_streams.sh) */
+#endif
 #ifndef FF_LONG
 #define FF_LONG 1           /* fast-forward runs past the 8-instruction window */
 #endif
@@ -1005,7 +1009,7 @@ sim_kernel(const SimArgs *Ap) {
                     const bool handoff = !FB && (st == DSM_RING_OVERFLOW);
                     const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
                     if (!handoff && !susp) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
-                    if (susp && ser_fmt) {    /* the serial pass's record (ssusp_words) */
+                    if (susp && ser_fmt && TRAFFIC_PROBE < 2) {    /* the serial pass's record (ssusp_words) */
                         uint32_t *sp = Ap->susp + sys * (uint64_t)ssusp_words(RING);
                         uint4 *mb = reinterpret_cast<uint4 *>(sp + 8u * node);     /* S_MB + 8 n */
                         mb[0] = make_uint4(s_mb[wv][0][lane], s_mb[wv][1][lane], s_mb[wv][2][lane], s_mb[wv][3][lane]);
@@ -2256,9 +2260,10 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
         if (ser) {
             /* the CAP build keeps per-node inbox counts for an inbox limit below 256 */
             const bool capb = c->inbox_limit < (uint32_t)FB_RING;
-            hipLaunchKernelGGL(np == 4 ? (capb ? ser_kernel<4, true> : ser_kernel<4, false>)
-                                       : (capb ? ser_kernel<8, true> : ser_kernel<8, false>),
-                               dim3(ser_blocks), dim3(64 * SER_WAVES), 0, st, a);
+            if (!TRAFFIC_PROBE)
+                hipLaunchKernelGGL(np == 4 ? (capb ? ser_kernel<4, true> : ser_kernel<4, false>)
+                                           : (capb ? ser_kernel<8, true> : ser_kernel<8, false>),
+                                   dim3(ser_blocks), dim3(64 * SER_WAVES), 0, st, a);
             HIPCK(hipGetLastError());
         } else if (pair) {
             hipLaunchKernelGGL(fast_nf, dim3(grid_fast), dim3(64 * FW), 0, st, a);
