@@ -31,7 +31,9 @@ for k, v in vals.items():
     per = collections.defaultdict(list)
     for (cname, _disp), xs in v.items():
         per[cname].append(sum(xs) * 1024.0)       # KB -> bytes, summed over the dispatch's rows
-    if k in ("sim_kernel", "ser_kernel"):
+    if k in ("sim_kernel", "ser_kernel", "parse_kernel"):
+        # (parse_kernel: the EXACT pass over the files the FAST pass abandoned -- none for the
+        # bench's generated text -- runs after each FAST pass and reads nothing)
         # the packed path launches a fast-forward / plain pair per pass and one of the two
         # exits at once (ffscan_kernel's verdict): average over the dispatches that ran
         per = {c: [x for x in xs if x >= (1 << 20)] or xs for c, xs in per.items()}
