@@ -1,5 +1,6 @@
-/* tests/native/parse_fast_equiv.cpp -- host check that parse_fast_swar (the chunk loop's decoder)
- * accepts exactly the chunks parse_fast accepts, with the same packed instruction, on canonical
+/* tests/native/parse_fast_equiv.cpp -- host check that parse_fast_v3 (the chunk loop's decoder) and
+ * parse_fast_swar accept exactly the chunks the byte-wise parse_fast accepts, with the same packed
+ * instruction, on canonical
  * "RD 0xHH\n" / "WR 0xHH D\n" lines mutated at random (tests/test_parse_swar.py). */
 #include <cstdint>
 #include <cstdio>

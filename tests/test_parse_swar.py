@@ -1,5 +1,6 @@
-"""parse_kernel's word-parallel chunk decoder (csrc/dsm_text.hip parse_fast_swar) against the
-byte-wise one it replaced in the chunk loop (parse_fast): both cut from the kernel source and
+"""parse_kernel's branch-free chunk decoder (csrc/dsm_text.hip parse_fast_v3, and the earlier
+word-parallel parse_fast_swar) against the byte-wise one they replaced in the chunk loop
+(parse_fast): all cut from the kernel source and
 compiled for the host, compared on 4M mutated canonical lines (reference: assignment.c:802-818,
 fgets + sscanf("RD %hhx") / sscanf("WR %hhx %hhu"); the exact slow path takes what they decline)."""
 import os
