@@ -183,6 +183,12 @@ struct Node {
     uint32_t nmsg;    /* messages handled                                                   */
 };
 
+/* global-address-space views: a generic (flat) access is counted in both vmcnt and lgkmcnt
+ * and completes out of order, so every later wait on memory, or on any LDS access, becomes
+ * vmcnt(0) lgkmcnt(0) while one is in flight */
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) uint32_t GU32;    /* global (not flat) accesses */
+typedef __attribute__((address_space(1))) v4u32 GV4;
 /* canonical 64-byte record (dsm_node_state) word i; mem / bv words come from LDS */
 DEVI uint32_t rec_word(const Node &nd, const uint32_t (&mb)[8], const uint32_t (&ln)[4], uint32_t flags, int i) {
     switch (i) {
@@ -246,9 +252,9 @@ DEVI uint64_t gsum64(uint64_t x) {
 /* 16-byte trace chunk load through the global address space: a generic (flat) load is
  * counted in both vmcnt and lgkmcnt and completes out of order, so every later wait on it,
  * or on any LDS access, becomes vmcnt(0) lgkmcnt(0). */
-typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) uint32_t GU32;    /* global (not flat) accesses */
-typedef __attribute__((address_space(1))) v4u32 GV4;
+DEVI uint32_t gatomic_add(GU32 *p, uint32_t v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 DEVI uint4 ld16(const uint16_t *p) {
     const v4u32 v = *(const __attribute__((address_space(1))) v4u32 *)p;
     return make_uint4(v.x, v.y, v.z, v.w);
@@ -1306,7 +1312,10 @@ ser_kernel(const SimArgs *Ap) {
     /* claim k -> system: last-suspended first, as the lock-step resume (whose records are the
      * likeliest still in the MALL; longest-first orders measured slower) */
     const uint32_t *const list = Ap->list;
-    auto sel = [&](uint32_t k) -> uint32_t { return list[n - 1 - k]; };
+    /* global (not flat) accesses: a pending flat operation makes every later wait a full
+     * vmcnt(0) lgkmcnt(0), the LDS waits of the macro-step included */
+    auto sel = [&](uint32_t k) -> uint32_t { return ((const GU32 *)list)[n - 1 - k]; };
+
     const uint32_t stride = Ap->stride, lim_rsh = Ap->lim_rsh, SR = Ap->susp_ring;
     const uint32_t cap = Ap->icap;
     const uint16_t *const traces = Ap->traces;
@@ -1333,12 +1342,11 @@ ser_kernel(const SimArgs *Ap) {
     uint4 cur = make_uint4(0, 0, 0, 0), nx = cur, pf = cur;
     auto slot_of = [&](uint32_t nd) { return traces + (sys * NP + nd) * (uint64_t)stride; };
 
-    auto claim = [&]() -> bool {
-        const uint32_t k = atomicAdd(claim_ctr, 1u);
-        if (k >= n) return false;
-        sys = sel(k);
-        return true;
+    auto claim_next = [&]() -> uint32_t {
+        return gatomic_add((GU32 *)claim_ctr, 1u);
     };
+
+
     /* the state the budget pass suspended, in serial form (ssusp_words): the LDS column as
      * it is, in 16-byte row loads (two batches of 12, all in flight at once), then the
      * per-node header -- ring position, trace length, messages received -- and each
@@ -1384,6 +1392,16 @@ ser_kernel(const SimArgs *Ap) {
         }
     };
     const bool serfmt = Ap->serfmt != 0u;   /* the format the budget pass wrote */
+    /* a serial-form record's 33 rows: the column (24) and the header (9), all in flight at
+     * once; issued before the finished system's record stores at a hand-over, so that the
+     * wait for them does not also wait for those stores (vmcnt counts both) */
+    v4u32 rr[33];
+    auto load_rec = [&](uint64_t s_) {
+        const GV4 *sv = (const GV4 *)(susp + s_ * (uint64_t)ssusp_words((int)SR));
+#pragma unroll
+        for (uint32_t i = 0; i < 33; ++i) rr[i] = sv[i];
+    };
+    /* start the system `sys` (its rows in rr when the budget pass wrote the serial form) */
     auto start = [&]() -> uint32_t {
         ser_clear(r);
         tn = 0xFFu;                         /* the fetch cache: empty */
@@ -1392,21 +1410,12 @@ ser_kernel(const SimArgs *Ap) {
             start_ls();
         } else {
         const GU32 *sp = (const GU32 *)(susp + sys * (uint64_t)ssusp_words((int)SR));
-        const GV4 *sv = (const GV4 *)sp;
 #pragma unroll
-        for (uint32_t bt = 0; bt < 2; ++bt) {
-            v4u32 x[12];
-#pragma unroll
-            for (uint32_t i = 0; i < 12; ++i) x[i] = sv[12u * bt + i];
-#pragma unroll
-            for (uint32_t i = 0; i < 12; ++i) {
-                const uint32_t w = 4u * (12u * bt + i);
-                m.st(w, x[i].x); m.st(w + 1u, x[i].y); m.st(w + 2u, x[i].z); m.st(w + 3u, x[i].w);
-            }
+        for (uint32_t i = 0; i < 24; ++i) {
+            const uint32_t w = 4u * i;
+            m.st(w, rr[i].x); m.st(w + 1u, rr[i].y); m.st(w + 2u, rr[i].z); m.st(w + 3u, rr[i].w);
         }
-        v4u32 hd[9];
-#pragma unroll
-        for (uint32_t i = 0; i < 9; ++i) hd[i] = sv[24u + i];
+        const v4u32 *const hd = rr + 24;
         r.rounds = hd[6].x;
         auto hw = [&](uint32_t k) -> uint32_t {        /* header word 96 + k, k < 24 (unrolled) */
             const v4u32 &v = hd[k >> 2];
@@ -1521,6 +1530,8 @@ ser_kernel(const SimArgs *Ap) {
         ins = (wd >> (16u * (j & 1u))) & 0xFFFFu;
         return have;
     };
+    bool live = false;
+    uint32_t v = SR_RUN;
     auto refill = [&]() {
         /* pf (chunk pfc, issued at an earlier refill) becomes nx once cur reaches pfc - 1;
          * then the chunk after the newest one held or in flight is requested, so two chunks
@@ -1541,13 +1552,14 @@ ser_kernel(const SimArgs *Ap) {
     auto on_dump = [&](uint32_t nd) { store_rec(nd, 2u, 0u); };
     auto finish = [&](uint32_t v) {
         if (v == SR_OVF) {               /* to the 256-deep re-run, from scratch */
-            const uint32_t pos = atomicAdd(ovf_count, 1u);
-            ovf_list[pos] = (uint32_t)sys;
+            const uint32_t pos = gatomic_add((GU32 *)ovf_count, 1u);
+            ((GU32 *)ovf_list)[pos] = (uint32_t)sys;
             atomicAdd(&s_cnt[K_OVFRERUN], 1ull);
             return;
         }
         uint32_t ins = 0;
-        for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {
+#pragma unroll
+        for (uint32_t nd = 0; nd < (uint32_t)NP; ++nd) {   /* unrolled: a fixed store count */
             ins += m.ld(S_CT + nd) >> SC_IP;
             store_rec(nd, ser_final_flags(m, nd), 1u);
         }
@@ -1562,8 +1574,13 @@ ser_kernel(const SimArgs *Ap) {
         atomicMax(&s_cnt[K_MAXR], (unsigned long long)r.rounds);
     };
 
-    bool live = claim();
-    uint32_t v = live ? start() : SR_RUN;
+    {
+        const uint32_t k = claim_next();
+        live = k < n;
+        if (live) sys = sel(k);
+        if (live && serfmt) load_rec(sys);
+    }
+    v = live ? start() : SR_RUN;
     uint32_t iters = 0, nmac = 0;
     for (;;) {
 #pragma unroll 1
@@ -1642,10 +1659,27 @@ ser_kernel(const SimArgs *Ap) {
             if (live && v != SR_RUN) {
                 uint64_t th0 = 0, th1 = 0, th2 = 0;
                 if (SER_PROBE >= 3) th0 = __builtin_amdgcn_s_memtime();
-                finish(v);
+                /* the successor: claimed and looked up first (waits that cover nothing but
+                 * older loads, the claim and the lookup), then its record's rows put in
+                 * flight before the finished system's record stores: the wait for the rows
+                 * (vmcnt counts stores too) is the only one left behind the stores.  Round 5:
+                 * C3 42.6 -> 40.4 ms, C5 32.6 -> 30.7 with the claim and the lookup as global,
+                 * not flat, accesses (a pending flat operation turns every later wait into a
+                 * full one) and the rows before the stores.  Measured slower, not kept:
+                 * claiming the successor ahead, at a refill step while the lone node's last
+                 * 16-64 instructions run (C5 31.9 ms); records written at their list position
+                 * so the claim needs no lookup (C3 +0.3 ms: the budget pass then waits for
+                 * the position before the record's stores). */
+                __builtin_amdgcn_s_waitcnt(0x0F70);             /* vmcnt(0) */
+                const uint32_t k = claim_next();
+                const bool nl = k < n;
+                const uint32_t ns = nl ? sel(k) : 0u;
+                if (nl && serfmt) load_rec(ns);
                 if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th1 = __builtin_amdgcn_s_memtime(); }
-                live = claim();
+                finish(v);
                 if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th2 = __builtin_amdgcn_s_memtime(); }
+                live = nl;
+                sys = ns;
                 v = live ? start() : SR_RUN;
                 if (SER_PROBE >= 3) {    /* hand-over cycles: finish, claim, start (lowest lane) */
                     __builtin_amdgcn_s_waitcnt(0);
