@@ -1251,6 +1251,12 @@ constexpr int SER_MACRO = SER_MACRO_DEF;   /* lone-node macro-steps per iteratio
 #ifndef SER_PROBE
 #define SER_PROBE 0
 #endif
+#ifndef SER_HB
+#define SER_HB 8            /* finished lanes that trigger a batched hand-over (1: at once) */
+#endif
+#ifndef SER_HT
+#define SER_HT 32           /* ... or iterations the oldest finished lane has waited */
+#endif
 
 template <int W>
 struct LdsCol {
@@ -1582,6 +1588,12 @@ ser_kernel(const SimArgs *Ap) {
     }
     v = live ? start() : SR_RUN;
     uint32_t iters = 0, nmac = 0;
+    /* batched hand-overs: a hand-over is a wave-wide phase (~19k cycles on C3, most of it
+     * waits on the claim, the lookup, the successor's rows and the record stores) however
+     * few lanes take part, so a finished system waits, its lane idle, until SER_HB lanes of
+     * the wave have finished, or the oldest has waited SER_HT iterations, or no running
+     * system is left in the wave; then they hand over together (wave-uniform) */
+    uint32_t hwait = 0;
     for (;;) {
 #pragma unroll 1
         for (int k = 0; k < SER_RF; ++k) {
@@ -1656,7 +1668,18 @@ ser_kernel(const SimArgs *Ap) {
                 const uint64_t hm = __ballot(live && v != SR_RUN);
                 if (lane == 0 && hm) atomicAdd(&s_cnt[4], 1ull);
             }
-            if (live && v != SR_RUN) {
+            bool hgo = false;
+            if (SER_HB > 1) {
+                const uint64_t fin = __ballot(live && v != SR_RUN);
+                if (fin) {
+                    hgo = (uint32_t)__builtin_popcountll(fin) >= (uint32_t)SER_HB ||
+                          hwait >= (uint32_t)SER_HT || fin == __ballot(live);
+                    hwait = hgo ? 0u : hwait + 1u;
+                }
+            } else {
+                hgo = true;
+            }
+            if (hgo && live && v != SR_RUN) {
                 uint64_t th0 = 0, th1 = 0, th2 = 0;
                 if (SER_PROBE >= 3) th0 = __builtin_amdgcn_s_memtime();
                 /* the successor: claimed and looked up first (waits that cover nothing but
