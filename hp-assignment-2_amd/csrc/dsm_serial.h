@@ -108,6 +108,16 @@ struct SReg {
 };
 
 DSM_HD uint32_t s_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
+/* some lane of the wave has c (the host model's one "lane": c) -- a wave-uniform branch
+ * around a load that most lanes take from registers (an LDS read under a per-lane select is
+ * issued for every lane and waited for on the chain) */
+DSM_HD bool s_any(bool c) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __ballot(c) != 0ull;
+#else
+    return c;
+#endif
+}
 /* b where bit k of n is set, else a -- by masks (v_bfi): a `?:` of two members of the
  * register struct is turned into a load from a selected address, which puts the whole
  * struct in scratch memory */
@@ -430,7 +440,11 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&sta
     constexpr uint32_t NPM = (1u << NP) - 1u;
     const uint32_t n = s_ctz(r.A), bit = 1u << n;
     const bool hot = cc.node == n;
-    uint32_t ct = hot ? cc.ct : m.ld(S_CT + n);
+    uint32_t ct = cc.ct;
+    if (s_any(!hot)) {
+        const uint32_t x = m.ld(S_CT + n);
+        ct = hot ? ct : x;
+    }
     const uint32_t ip = ct >> SC_IP;
     if (ip >= s_ni(r, n)) {
         /* the trace is done: the dump (:688-697), the round's one action; then no node can
@@ -453,7 +467,12 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&sta
     stamp(0);
     const uint32_t a = (ins >> 8) & 0x7Fu, wr = ins >> 15, val = ins & 0xFFu;
     const uint32_t h = a >> 4, b = a & 15u, idx = a & 3u, sh8 = 8u * idx;
-    const uint32_t laW = hot ? cc.la : m.ld(S_LA + n), lvW = hot ? cc.lv : m.ld(S_LV + n);
+    uint32_t laW = cc.la, lvW = cc.lv;
+    if (s_any(!hot)) {
+        const uint32_t x = m.ld(S_LA + n), y = m.ld(S_LV + n);
+        laW = hot ? laW : x;
+        lvW = hot ? lvW : y;
+    }
     const uint32_t La = (laW >> sh8) & 0xFFu, Lv = (lvW >> sh8) & 0xFFu;
     const uint32_t lsh = SC_LS + 2u * idx, Ls = (ct >> lsh) & 3u;          /* M0 E1 S2 I3 */
     const bool hit = (La == a) & (Ls != 3u);                   /* :608, :635 */
@@ -508,11 +527,12 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&sta
     const uint32_t o = owner & 7u;
     bool oflush = false;
     uint32_t ctO = 0u, vO = 0u;                                 /* o's control word, the value it flushes */
-    if (fwd) {            /* rare: the owner's line, read only then (a dependent LDS level) */
+    if (s_any(fwd)) {     /* rare: the owner's line, read only then (a dependent LDS level) */
         const uint32_t laO = m.ld(S_LA + o), lvO = m.ld(S_LV + o);
-        ctO = m.ld(S_CT + o);
-        oflush = (((laO >> sh8) & 0xFFu) == a) & (((ctO >> lsh) & 3u) <= 1u);
-        vO = (lvO >> sh8) & 0xFFu;
+        const uint32_t c0 = m.ld(S_CT + o);
+        ctO = fwd ? c0 : 0u;
+        oflush = fwd & (((laO >> sh8) & 0xFFu) == a) & (((c0 >> lsh) & 3u) <= 1u);
+        vO = fwd ? (lvO >> sh8) & 0xFFu : 0u;
     }
     /* a forward to an owner that no longer holds the block in M or E: the owner ignores it
      * (:266-270, :468-472), no flush comes and the requester waits for good -- the system's
@@ -550,9 +570,9 @@ DSM_HD bool ser_macro(M &m, SReg &r, SCache &cc, F &&fetch, R &&on_dump, P &&sta
     /* the forward's owner: S after FLUSH, I after FLUSH_INVACK */
     m.st_if(fwd & !dead, S_CT + o, (ctO & ~(3u << lsh)) | ((wr ? 3u : 2u) << lsh));
     /* the notice's target: its line (same index) S -> E when it still holds the victim */
-    if (notice & !selfn) {
+    if (s_any(notice & !selfn)) {
         const uint32_t laX = m.ld(S_LA + x), ctX = m.ld(S_CT + x);
-        const bool up = (((laX >> sh8) & 0xFFu) == La) & (((ctX >> lsh) & 3u) == 2u);
+        const bool up = notice & !selfn & (((laX >> sh8) & 0xFFu) == La) & (((ctX >> lsh) & 3u) == 2u);
         m.st_if(up, S_CT + x, (ctX & ~(3u << lsh)) | (1u << lsh));
     }
     /* the fan-out's sharers: a line holding the block in S or E becomes INVALID */
