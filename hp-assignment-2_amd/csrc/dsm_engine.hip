@@ -1549,7 +1549,7 @@ ser_kernel(const SimArgs *Ap) {
         }
         if (pfv && (pfc <= tci || pfc > tci + 2u)) pfv = false;     /* stale: a jump */
         const uint32_t want = nxv ? tci + 2u : tci + 1u;
-        if (tn != 0xFFu && !pfv && want * 8u < stride) {
+        if (tn != 0xFFu && !pfv && want * 8u < stride && v == SR_RUN) {   /* not while it waits to hand over */
             pf = ld16(slot_of(tn) + want * 8u);
             pfc = want;
             pfv = true;
