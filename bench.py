@@ -328,6 +328,91 @@ def issue_from_profiles(config):
     return _load_json(os.path.join(REPO, "profiles", "pmc_issue.json")).get(config) or None
 
 
+def run_c_driver(args):
+    """bench.py --driver c: the C multi-GPU driver (hp-assignment-2_amd/dsm_ensemble: one
+    process, one host thread per GPU, RCCL all-reduce through dsm_group_*) over N GPUs; its
+    per-rank aggregates, job total, counters and per-type counts are checked here against the
+    reference's, and the bench line is printed from its JSON.  Returns the exit code (3 on a
+    parity mismatch)."""
+    import pydsm
+    dname, n_sys, n_instr, seed, workload = CONFIGS[args.config]
+    if args.systems:
+        n_sys = args.systems
+    cmd = [os.path.join(PKG, "dsm_ensemble"), "--gpus", str(args.gpus), "--config", args.config,
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--systems", str(n_sys)]
+    if not args.no_types:
+        cmd.append("--type-counts")
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    sys.stderr.write(r.stderr)
+    if r.returncode != 0:
+        return r.returncode
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    tally = dict(ok=0, bad=0, unpinned=0)
+    for rk in d["ranks"]:
+        gold, src = golden_for(dname, seed, n_instr, rk["first_sys"], rk["systems"])
+        if gold is None:
+            tally["unpinned"] += 1
+            continue
+        diff = pydsm.aggregate_diff(rk["aggregate"], gold)
+        tally["bad" if diff else "ok"] += 1
+        print(f"bench.py --driver c: rank {rk['rank']} shard [{rk['first_sys']}, "
+              f"{rk['first_sys'] + rk['systems']}) " +
+              (f"== reference ({src})" if not diff else f"MISMATCH vs {src}: " + ",".join(diff)),
+              file=sys.stderr, flush=True)
+    world = d["n_gpus"]
+    counters = dict(d["counters"], sum_final_hash=int(d["counters"]["sum_final_hash"], 16))
+    gold, src = golden_for(dname, seed, n_instr, 0, world * n_sys)
+    if gold is None:
+        parity = f"job total over {world} shard(s) unpinned"
+    else:
+        diff = check_aggregate(d["total"], gold, counters)
+        parity = (f"full-size aggregate == reference (job total over {world} shard(s), {src})"
+                  if not diff else f"AGGREGATE MISMATCH vs {src}: " + ",".join(diff))
+    parity += f"; {tally['ok']}/{world} shards == their reference aggregates"
+    if tally["bad"]:
+        parity += f"; {tally['bad']} SHARD MISMATCH"
+    by_type = d.get("msgs_by_type")
+    if by_type is not None:
+        if sum(by_type) != counters["msgs"] or d.get("type_pass_msgs") != counters["msgs"]:
+            parity += "; MSGS_BY_TYPE MISMATCH (sum != messages)"
+        elif gold is not None and gold.get("msgs_by_type"):
+            parity += ("; msgs_by_type == reference (13 types)" if by_type == gold["msgs_by_type"]
+                       else "; MSGS_BY_TYPE MISMATCH vs reference")
+    kavg = float(np.mean(d["kernel_ms"])) if d["kernel_ms"] else float("nan")
+    r0 = d["ranks"][0]["aggregate"]
+    alg_bytes = 2 * r0["instrs"] + (32 + 4 * NP) * r0["systems"]
+    ach = alg_bytes / (kavg * 1e-3) / 1e9
+    tr = traffic_from_profiles(args.config) or {}
+    traffic = None
+    if tr.get("sim_kernel") and tr.get("ser_kernel"):
+        traffic = int(tr["sim_kernel"]["bytes_per_launch"] + tr["ser_kernel"]["bytes_per_launch"])
+    rec = {
+        "metric": METRIC, "value": d["value"], "unit": UNIT, "n_gpus": world,
+        "steps": d["steps"], "warmup": d["warmup"], "ms_per_step": d["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (counter-based generator, seed %d)" % seed,
+        "config": {"workload": workload, "systems_per_gpu": n_sys, "np": NP,
+                   "instr_per_node": n_instr, "dist": dname,
+                   "parallelism": f"ensemble-dp{world} (C driver: one host thread per GPU)",
+                   "traces": "packed u16 traces resident in HBM"},
+        "roofline": dict(bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                         frac=round(ach / HBM_PEAK_GBS, 6), traffic=traffic,
+                         kernel_ms_avg=round(kavg, 3), algorithmic_bytes_per_launch=alg_bytes,
+                         per_unit="2 B per consumed packed instruction + 32 B result + 4*np B "
+                                  "counts per system; 'launch' = one step's budget + resume launches"),
+        "cpu_baseline": None,
+        "driver": d["driver"],
+        "collective": d["collective"],
+        "counters": d["counters"],
+        "msgs_by_type": dict(zip(pydsm.TYPE_NAMES, by_type)) if by_type is not None else None,
+        "kernel_ms": d["kernel_ms"],
+        "parity": parity,
+        "parity_detail": dict(job_source=src, shards=tally),
+    }
+    print(json.dumps(rec), flush=True)
+    return 3 if "MISMATCH" in parity else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -346,8 +431,18 @@ def main():
     ap.add_argument("--no-dump", action="store_true", help="skip the GPU dump-formatter phase")
     ap.add_argument("--parse-systems", type=int, default=65536,
                     help="systems whose core files are generated as text and GPU-parsed (0: skip)")
+    ap.add_argument("--no-types", action="store_true",
+                    help="skip the per-type message count pass (parity only, after timing)")
+    ap.add_argument("--driver", default="py", choices=("py", "c"),
+                    help="c: the C multi-GPU driver (hp-assignment-2_amd/dsm_ensemble: one host "
+                         "thread per GPU, RCCL), checked here against the reference aggregates")
     args = ap.parse_args()
 
+    if args.driver == "c":
+        if "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+            raise SystemExit("bench.py --driver c runs every GPU from one process: launch it "
+                             "without torchrun")
+        sys.exit(run_c_driver(args))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one fresh process per GPU, started before this process touches the GPU
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -364,19 +459,23 @@ def main():
     # test knobs (tests/test_gpu_bench.py): every rank on one device, gloo for the counters
     if os.environ.get("DSM_BENCH_DEVICE"):
         local = int(os.environ["DSM_BENCH_DEVICE"])
-    backend = os.environ.get("DSM_BENCH_BACKEND", "nccl")     # nccl = RCCL over xGMI
-    # DSM_BENCH_DIST=1: the process group and its collectives even at one rank -- on a
-    # one-GPU box that runs the RCCL init / barrier / all-reduce path end to end
-    use_dist = world > 1 or os.environ.get("DSM_BENCH_DIST") == "1"
+    # nccl (default): the collectives are RCCL over xGMI issued by libdsm itself (dsm_group_*,
+    # one communicator per GPU, even at one rank); torch.distributed (gloo, CPU) only hands
+    # rank 0's RCCL id to the other ranks.  gloo (tests: several ranks on one GPU, which RCCL
+    # refuses): the collectives through a torch.distributed gloo group on host tensors.
+    backend = os.environ.get("DSM_BENCH_BACKEND", "nccl")
+    use_group = backend == "nccl"
+    use_dist = world > 1 or (not use_group and os.environ.get("DSM_BENCH_DIST") == "1")
+    torch.cuda.set_device(local)
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")
+    group = None
+    if use_group:
+        uid = [pydsm.Group.unique_id() if rank == 0 else None]
+        if use_dist:
+            dist.broadcast_object_list(uid, src=0)
+        group = pydsm.Group(local, world, rank, uid[0])
 
     dname, n_sys, n_instr, seed, workload = CONFIGS[args.config]
     if args.systems:
@@ -415,22 +514,25 @@ def main():
             eng.run_generated_device(dname, seed, n_instr, first, n_sys, out.data_ptr(),
                                      cnt.data_ptr(), sp)
         else:
-            eng.run_packed_device(traces.data_ptr(), counts.data_ptr(), n_sys, out.data_ptr(),
-                                  cnt.data_ptr(), sp)
+            eng.run_packed_device(traces, counts, n_sys, out, cnt, sp)
+
+    def barrier():
+        if group is not None:
+            group.barrier(sp)           # RCCL all-reduce of one word, then a stream wait
+        elif use_dist:
+            dist.barrier()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
 
-    if use_dist:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()          # asynchronous: the steps queue back to back on the stream
     torch.cuda.synchronize(dev)
-    if use_dist:
-        dist.barrier()
+    barrier()
     elapsed = time.perf_counter() - t0
     # the transition kernel's device time per step (HIP events around its launches, on the
     # stream they run on), read after the timed region
@@ -499,14 +601,50 @@ def main():
                            frac=round(fbytes / fms / 1e6 / HBM_PEAK_GBS, 4))
         del d_txt, d_len
 
-    cdev = dev if backend == "nccl" else torch.device("cpu")    # gloo: host tensors
-    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-    if use_dist:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed_max = float(el.item())
+    cdev = torch.device("cpu")                                  # gloo: host tensors
+
+    def allreduce_counters(t):
+        """A device dsm_counters vector summed over ranks (max for max_rounds), as a dict."""
+        if group is not None:
+            t = t.clone()
+            group.allreduce_counters(t, sp)
+            torch.cuda.synchronize(dev)
+        else:
+            t = reduce_counters(t.clone().to(cdev), dist if use_dist else None)
+        return pydsm.counters_to_dict(t.cpu().numpy().view(np.uint64))
+
+    if group is not None:
+        el = torch.tensor([int(elapsed * 1e9)], dtype=torch.int64, device=dev)
+        group.allreduce(el, 1, pydsm.RED_MAX, sp)
+        torch.cuda.synchronize(dev)
+        elapsed_max = int(el.item()) * 1e-9
+    else:
+        el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        if use_dist:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed_max = float(el.item())
     local_c = pydsm.counters_to_dict(cnt.cpu().numpy().view(np.uint64))
-    tot = reduce_counters(cnt.clone().to(cdev), dist if use_dist else None)
-    c = pydsm.counters_to_dict(tot.cpu().numpy().view(np.uint64))
+    c = allreduce_counters(cnt)
+
+    # handled messages per transactionType (assignment.c:20-34), parity only: the timed
+    # kernels do not count types, so the same traces run once more, untimed, on a context
+    # with DSM_F_TYPE_COUNTS (the one-pass lock-step kernel with per-type counters); its
+    # totals must equal the timed run's messages and the reference's per-type totals
+    type_pass = None
+    if not args.fused and not args.no_types:
+        teng = pydsm.Engine(NP, n_instr, ring_cap=args.ring, device=local, type_counts=True)
+        tcnt = torch.zeros(pydsm.NCOUNTERS, dtype=torch.int64, device=dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        teng.run_packed_device(traces, counts, n_sys, None, tcnt, sp)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        tli = teng.launch_info()
+        teng.close()
+        tc = allreduce_counters(tcnt)
+        type_pass = dict(msgs_by_type=[tc[f"msgs_{t}"] for t in pydsm.TYPE_NAMES],
+                         msgs=tc["msgs"], ms=round(e0.elapsed_time(e1), 3),
+                         kernel=tli["kernels"] + " with DSM_F_TYPE_COUNTS (parity only, untimed)")
 
     # parity after the timed region, on every rank: the last step's per-system results of this
     # rank's shard against the reference's own handler text (its full-size aggregate:
@@ -514,11 +652,36 @@ def main():
     # all-reduced aggregate against the reference's total over ids [0, world * n)
     res_host = out.cpu().numpy().view(pydsm.RESULT_DTYPE).reshape(-1)
     mine, verdict, shard_msg = shard_parity(dname, seed, n_instr, first, res_host, local_c)
+    # the library's device fold of the same results (dsm_aggregate_device, what the C driver
+    # all-reduces) must equal the host fold
+    agg_dev = torch.zeros(pydsm.NAGG, dtype=torch.int64, device=dev)
+    eng.aggregate_device(out, n_sys, first, agg_dev, sp)
+    torch.cuda.synchronize(dev)
+    dev_diff = pydsm.aggregate_diff(pydsm.agg_vec_to_dict(agg_dev.cpu().numpy().view(np.uint64)), mine)
+    if dev_diff:
+        verdict = "bad"
+        shard_msg += "; DEVICE AGGREGATE MISMATCH: " + ",".join(dev_diff)
     print(f"bench.py rank {rank}: {shard_msg}", file=sys.stderr, flush=True)
-    avec = torch.from_numpy(agg_to_vec(mine, verdict).view(np.int64).copy()).to(cdev)
-    avec = reduce_vector(avec, dist if use_dist else None, (AGG_MAX,))
+    avec = torch.from_numpy(agg_to_vec(mine, verdict).view(np.int64).copy())
+    if group is not None:       # dsm_aggregate layout: the shard tallies ride in its reserved slots
+        avec = avec.to(dev)
+        group.allreduce_aggregate(avec, sp)
+        torch.cuda.synchronize(dev)
+    else:
+        avec = reduce_vector(avec.to(cdev), dist if use_dist else None, (AGG_MAX,))
     parity, parity_detail = job_parity(dname, seed, n_instr, world, n_sys,
                                        avec.cpu().numpy().view(np.uint64), c)
+    if type_pass is not None:
+        gold, _ = golden_for(dname, seed, n_instr, 0, world * n_sys)
+        ok_sum = sum(type_pass["msgs_by_type"]) == c["msgs"] == type_pass["msgs"]
+        if not ok_sum:
+            parity += "; MSGS_BY_TYPE MISMATCH (sum != messages)"
+        elif gold is not None and gold.get("msgs_by_type"):
+            parity += ("; msgs_by_type == reference (13 types)"
+                       if type_pass["msgs_by_type"] == gold["msgs_by_type"]
+                       else "; MSGS_BY_TYPE MISMATCH vs reference")
+        else:
+            parity += "; msgs_by_type sums to messages (no reference per-type totals)"
 
     if rank == 0:
         K = args.steps
@@ -639,18 +802,27 @@ def main():
                                            "ff_passes", "ff_steps", "ff_sample_instrs",
                                            "ff_sample_runs", "ser_macro_steps", "status_COMPLETED",
                                            "status_DEADLOCKED")},
+            "msgs_by_type": dict(zip(pydsm.TYPE_NAMES, type_pass["msgs_by_type"])) if type_pass else None,
+            "type_pass": {k: v for k, v in (type_pass or {}).items() if k != "msgs_by_type"} or None,
             "kernel_ms": [round(x, 3) for x in kms],
             "sum_final_hash": hex(c["sum_final_hash"]),
             "parity": parity,
             "parity_detail": parity_detail,
-            "collective": (("rccl" if backend == "nccl" else backend) + f" all_reduce of {pydsm.NCOUNTERS} counters over {world} rank(s)")
-                          if use_dist else None,
+            "collective": (f"rccl ncclAllReduce issued by libdsm (dsm_group_*: counters, aggregate, "
+                           f"elapsed max, barriers) over {world} rank(s)" if group is not None else
+                           f"{backend} all_reduce of {pydsm.NCOUNTERS} counters over {world} rank(s)"
+                           if use_dist else None),
             "launch": eng.launch_info(),
         }
         print(json.dumps(rec), flush=True)
     eng.close()
+    if group is not None:
+        group.close()
     if use_dist:
         dist.destroy_process_group()
+    # a failed parity check fails the run: this rank's shard, and on rank 0 the job's line
+    if verdict == "bad" or (rank == 0 and "MISMATCH" in parity):
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -36,6 +36,10 @@
 #include <string.h>
 
 #include "dsm.h"
+#ifndef SIM_BF
+#define SIM_BF 0            /* A/B: bit 0 the first receive-mask ORs without a branch, bit 1 the
+                               first destination index as a mask select (dsm_table.h) */
+#endif
 #include "dsm_table.h"
 #include "dsm_internal.h"
 #include "dsm_gen.h"
@@ -105,9 +109,21 @@ struct SimArgsPack { SimArgs a[3]; };
 
 #define DEVI __device__ __forceinline__
 
+/* s_waitcnt vmcnt(0) with expcnt / lgkmcnt left open, as the raw immediate of the gfx9 encoding
+ * (vmcnt bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8): it means something else on gfx10+,
+ * and this library is built for gfx950 only */
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "dsm_engine.hip targets gfx950 (raw gfx9 s_waitcnt encodings)"
+#endif
+DEVI void wait_vmcnt0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 #ifndef TRAFFIC_PROBE
 #define TRAFFIC_PROBE 0     /* traffic attribution builds (results invalid): 1 no serial pass, 2 and
                                no serial-form suspend records (tools/traffic_streams.sh) */
+#endif
+#ifndef SIM_TAILPROBE
+#define SIM_TAILPROBE 0     /* budget-pass wave end-time histogram (probe build, results exact;
+                               tools/tail_probe.py) */
 #endif
 #ifndef FF_LONG
 #define FF_LONG 1           /* fast-forward runs past the 8-instruction window */
@@ -462,6 +478,9 @@ sim_kernel(const SimArgs *Ap) {
     s_rm[wv][lane] = 0;
     for (uint32_t i = threadIdx.x; i < DT_TABLE_WORDS / 2; i += 64 * WAVES) s_tab[i] = Ap->table[i];
     __syncthreads();
+#if SIM_TAILPROBE
+    const uint64_t tprobe0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     const uint64_t n = Ap->d_n ? (uint64_t)*Ap->d_n : Ap->n_sys;
     const uint32_t *list = Ap->list;
@@ -575,7 +594,7 @@ sim_kernel(const SimArgs *Ap) {
             const uint4 v0 = ld16(tb), v1 = ld16(tb + (stride > 8 ? 8 : 0));
             cur[0] = v0.x; cur[1] = v0.y; cur[2] = v0.z; cur[3] = v0.w;
             nxt[0] = v1.x; nxt[1] = v1.y; nxt[2] = v1.z; nxt[3] = v1.w;
-            __builtin_amdgcn_s_waitcnt(0x0F70);                 /* vmcnt(0) */
+            wait_vmcnt0();
         }
     };
 
@@ -924,8 +943,17 @@ sim_kernel(const SimArgs *Ap) {
                 uint32_t m0 = o0 >> 24, m1 = o1 >> 24;
                 const uint32_t b0 = 2 * node;
                 const uint32_t bit0 = 1u << b0, bit1 = 2u << b0;
+#if SIM_BF & 1
+                /* each word's first destination without a branch: a lane with none ORs 0 into
+                 * its own mask */
+                atomicOr(&s_rm[wv][m0 ? gbase + __builtin_ctz(m0) : lane], m0 ? bit0 : 0u);
+                atomicOr(&s_rm[wv][m1 ? gbase + __builtin_ctz(m1) : lane], m1 ? bit1 : 0u);
+                m0 &= m0 - 1;
+                m1 &= m1 - 1;
+#else
                 if (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
                 if (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
+#endif
                 while (m0) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m0)], bit0); m0 &= m0 - 1; }
                 while (m1) { atomicOr(&s_rm[wv][gbase + __builtin_ctz(m1)], bit1); m1 &= m1 - 1; }
             }
@@ -1201,6 +1229,17 @@ sim_kernel(const SimArgs *Ap) {
      * depend on the order, so no separate reduction pass is needed) */
     if (lane == 0) {
         s_cnt[wv][K_WROUNDS] = wrounds;
+#if SIM_TAILPROBE
+        /* probe build (results exact, not the default): when the budget pass's waves end, a
+         * histogram in the msgs_by_type slots -- 0: before 14 ms, k = 1..11: [13 + k, 14 + k)
+         * ms, 12: the waves' summed lifetimes in 10-ns ticks (s_memrealtime, 100 MHz) */
+        if (BUD && budget) {
+            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - tprobe0;
+            const uint64_t ms = dt / 100000u;
+            s_cnt[wv][ms < 14u ? 0u : (ms - 13u < 11u ? ms - 13u : 11u)] += 1;
+            s_cnt[wv][12] += dt;
+        }
+#endif
     }
     __syncthreads();
     if (threadIdx.x < K_N) {
@@ -1507,7 +1546,7 @@ ser_kernel(const SimArgs *Ap) {
             }
             /* wait here, in the rare branch: left to the first use after the join, the wait
              * (vmcnt(0)) lands on the main path and also waits for the refill's prefetches */
-            __builtin_amdgcn_s_waitcnt(0x0F70);             /* vmcnt(0) */
+            wait_vmcnt0();
         }
         /* word (ip & 7) / 2 of cur by masks: a select chain on a run-time index is turned
          * into a stack copy and an indexed scratch load */
@@ -1693,7 +1732,7 @@ ser_kernel(const SimArgs *Ap) {
                  * 16-64 instructions run (C5 31.9 ms); records written at their list position
                  * so the claim needs no lookup (C3 +0.3 ms: the budget pass then waits for
                  * the position before the record's stores). */
-                __builtin_amdgcn_s_waitcnt(0x0F70);             /* vmcnt(0) */
+                wait_vmcnt0();
                 const uint32_t k = claim_next();
                 const bool nl = k < n;
                 const uint32_t ns = nl ? sel(k) : 0u;
@@ -1742,6 +1781,54 @@ ser_kernel(const SimArgs *Ap) {
             if (threadIdx.x == K_MAXR) atomicMax(&Ap->counters[K_MAXR], x);
             else atomicAdd(&Ap->counters[threadIdx.x], x);
         }
+    }
+}
+
+/* ---- aggregate: the golden-aggregate view of per-system results (dsm_aggregate) --------
+ * One lane per system (32-B result: two 16-B loads); per-lane sums, then wave sums by
+ * shuffles and one device atomic per slot and workgroup.  The result digest is the sum of
+ * per-system fmix64 chains over the absolute system id (dsm_host.c dsm_result_digest). */
+constexpr int AGG_SLOTS = 13;      /* systems, msgs, instrs, rounds, max, status x5, dh, fh, digest */
+static_assert(AGG_SLOTS <= DSM_NAGG && DSM_AGG_MAX_SLOT == 4, "dsm_aggregate layout");
+__global__ void __launch_bounds__(256) agg_kernel(uint64_t n_sys, uint64_t first_sys,
+                                                  const uint4 *res, unsigned long long *agg) {
+    __shared__ unsigned long long s_a[4][AGG_SLOTS];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint64_t v[AGG_SLOTS];
+#pragma unroll
+    for (int k = 0; k < AGG_SLOTS; ++k) v[k] = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n_sys; i += (uint64_t)gridDim.x * 256) {
+        const uint4 a = res[2 * i], b = res[2 * i + 1];
+        const uint64_t dh = b.x | ((uint64_t)b.y << 32), fh = b.z | ((uint64_t)b.w << 32);
+        const uint32_t st = a.x & 0xFFu;
+        v[0] += 1; v[1] += a.z; v[2] += a.w; v[3] += a.y;
+        v[4] = a.y > v[4] ? a.y : v[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 5; ++k) v[5 + k] += st == k ? 1u : 0u;
+        v[10] += dh; v[11] += fh;
+        uint64_t h = fmix64((first_sys + i) * 0x9E3779B97F4A7C15ULL + 1u);
+        h = fmix64(h ^ ((uint64_t)a.x | ((uint64_t)a.y << 32)));
+        h = fmix64(h ^ ((uint64_t)a.z | ((uint64_t)a.w << 32)));
+        h = fmix64(h ^ dh);
+        v[12] += fmix64(h ^ fh);
+    }
+#pragma unroll
+    for (int k = 0; k < AGG_SLOTS; ++k) {
+        uint64_t x = v[k];
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t lo = __shfl_xor((uint32_t)x, o, 64), hi = __shfl_xor((uint32_t)(x >> 32), o, 64);
+            const uint64_t y = ((uint64_t)hi << 32) | lo;
+            x = k == 4 ? (y > x ? y : x) : x + y;
+        }
+        if (lane == 0) s_a[wv][k] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < AGG_SLOTS) {
+        const uint32_t k = threadIdx.x;
+        unsigned long long x = s_a[0][k];
+        for (int w = 1; w < 4; ++w) x = k == 4 ? (s_a[w][k] > x ? s_a[w][k] : x) : x + s_a[w][k];
+        if (k == 4) atomicMax(&agg[k], x);
+        else if (x) atomicAdd(&agg[k], x);
     }
 }
 
@@ -2086,6 +2173,32 @@ extern "C" int dsm_launch_info_get(dsm_ctx *c, dsm_launch_info *info) {
     return DSM_OK;
 }
 
+/* the non-default compile-time knobs of this build ("" for the default build): A/B and probe
+ * variants (tools/build_variant.sh) label their launches apart, and a probe build whose
+ * results are not valid for timing (TRAFFIC_PROBE, SIM_TAILPROBE, SER_PROBE) says so */
+static const char *build_variant() {
+    static char tag[160];
+    if (tag[0]) return tag[1] ? tag + 1 : "";
+    int n = snprintf(tag, sizeof tag, "#");
+    auto add = [&](const char *name, long v, long def) {
+        if (v != def && n < (int)sizeof tag) n += snprintf(tag + n, sizeof tag - n, " %s=%ld", name, v);
+    };
+    add("SIM_BF", SIM_BF, 0);
+    add("SIM_TAILPROBE", SIM_TAILPROBE, 0);
+    add("TRAFFIC_PROBE", TRAFFIC_PROBE, 0);
+    add("SER_PROBE", SER_PROBE, 0);
+    add("SER_HB", SER_HB, 8);
+    add("SER_HT", SER_HT, 32);
+    add("SER_RF_DEF", SER_RF_DEF, 8);
+    add("SER_MACRO_DEF", SER_MACRO_DEF, 1);
+    add("FF_LONG", FF_LONG, 1);
+    add("FF_LONG_U", FF_LONG_U, 8);
+    add("SER_DEAD_FWD", SER_DEAD_FWD, 1);
+    add("SER_NOTICE_HOME", SER_NOTICE_HOME, 1);
+    add("SER_DUMP", SER_DUMP, 0);
+    return tag[1] ? tag + 1 : "";
+}
+
 extern "C" int dsm_launch_kernel_names(const dsm_launch_info *info, char *buf, size_t cap) {
     if (!info || !buf) return DSM_E_INVAL;
     char b[2][96];
@@ -2105,6 +2218,8 @@ extern "C" int dsm_launch_kernel_names(const dsm_launch_info *info, char *buf, s
         else snprintf(b[1], 96, "ser_kernel<%d, %s>", info->np, info->ser_cap ? "true" : "false");
         n = snprintf(buf, cap, "budget=%s resume=%s", b[0], b[1]);
     }
+    const char *v = build_variant();
+    if (n >= 0 && *v && (size_t)n < cap) n += snprintf(buf + n, cap - n, " [variant:%s]", v);
     return (n < 0 || (size_t)n >= cap) ? DSM_E_INVAL : n;
 }
 
@@ -2480,6 +2595,20 @@ extern "C" int dsm_generate_device(dsm_ctx *c, const dsm_gen *g, uint64_t first_
          {gen_kernel<8, 2, false>, gen_kernel<8, 2, true>}}};
     hipLaunchKernelGGL(tab[np == 8][g->dist][full], dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream,
                        g->seed, g->dist, first_sys, n_sys, g->n_instr, c->cfg.max_instr, d_traces, d_counts);
+    HIPCK(hipGetLastError());
+    return DSM_OK;
+}
+
+extern "C" int dsm_aggregate_device(dsm_ctx *c, const dsm_sys_result *d_results, uint64_t n_sys,
+                                    uint64_t first_sys, dsm_aggregate *d_agg, void *stream) {
+    if (!c || !d_agg || (n_sys && !d_results)) return DSM_E_INVAL;
+    if (n_sys == 0) return DSM_OK;
+    HIPCK(hipSetDevice(c->device));
+    uint64_t blocks = (n_sys + 255) / 256;
+    const uint64_t cap = (uint64_t)c->cus * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(agg_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n_sys, first_sys,
+                       reinterpret_cast<const uint4 *>(d_results), reinterpret_cast<unsigned long long *>(d_agg));
     HIPCK(hipGetLastError());
     return DSM_OK;
 }

@@ -155,3 +155,33 @@ uint64_t dsm_node_hash(int node, const dsm_node_state *st, int nwords) {
     for (int i = 0; i < nwords; ++i) h = fmix64(h ^ ((uint64_t)w[i] | ((uint64_t)i << 32)));
     return h;
 }
+
+/* one system's term of the aggregate's result digest: a fmix64 chain over the absolute
+ * system id and the six result fields (position-sensitive, so a sum of terms pins every
+ * system's result, and shards merge by addition) */
+uint64_t dsm_result_digest(uint64_t sys_id, const dsm_sys_result *r) {
+    uint64_t h = fmix64(sys_id * 0x9E3779B97F4A7C15ULL + 1u);
+    h = fmix64(h ^ ((uint64_t)r->status | ((uint64_t)r->rounds << 32)));
+    h = fmix64(h ^ ((uint64_t)r->msgs | ((uint64_t)r->instrs << 32)));
+    h = fmix64(h ^ r->dump_hash);
+    return fmix64(h ^ r->final_hash);
+}
+
+int dsm_aggregate_results(const dsm_sys_result *res, uint64_t n_sys, uint64_t first_sys,
+                          dsm_aggregate *agg) {
+    if (!agg || (n_sys && !res)) return DSM_E_INVAL;
+    memset(agg, 0, sizeof *agg);
+    for (uint64_t i = 0; i < n_sys; ++i) {
+        const dsm_sys_result *r = &res[i];
+        agg->systems++;
+        agg->msgs += r->msgs;
+        agg->instrs += r->instrs;
+        agg->rounds += r->rounds;
+        if (r->rounds > agg->max_rounds) agg->max_rounds = r->rounds;
+        if ((r->status & 0xFFu) < 5u) agg->by_status[r->status & 0xFFu]++;
+        agg->sum_dump_hash += r->dump_hash;
+        agg->sum_final_hash += r->final_hash;
+        agg->result_digest += dsm_result_digest(first_sys + i, r);
+    }
+    return DSM_OK;
+}

@@ -435,7 +435,12 @@ DSM_HD DtOut dt_apply_xy(const DtIn &in, uint32_t X, uint32_t Y, uint32_t W0, ui
     const bool d0 = dc & 1u, d1 = dc & 2u, d2 = dc & 4u;
     const uint32_t ctzEv = (uint32_t)__builtin_ctz((evDb & in.np_mask) | 0x80000000u);
     const uint32_t own = (uint32_t)__builtin_ctz((in.Db & in.np_mask) | 0x80000000u);  /* findOwner */
+#if defined(SIM_BF) && (SIM_BF & 2)
+    const uint32_t m1s = 0u - (uint32_t)d1;                    /* no branch on d1 */
+    const uint32_t didx = ((d0 ? ctzEv : (in.La >> 4)) & m1s) | ((d0 ? own : in.s) & ~m1s);
+#else
     const uint32_t didx = d1 ? (d0 ? ctzEv : (in.La >> 4)) : (d0 ? own : in.s);
+#endif
     const uint32_t mset = d0 ? (in.v & in.np_mask & ~(1u << in.node)) : ((1u << H) | (1u << in.r2));
     const uint32_t dm = d2 ? mset : (1u << didx);
     /* a word is sent iff its destination mask is non-zero; the body of an unsent word is

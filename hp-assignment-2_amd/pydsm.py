@@ -128,6 +128,19 @@ def lib():
             "dsm_parse_traces_device": (i32, [vp, vp, vp, u64, u32, vp, vp, vp, vp]),
             "dsm_parse_traces": (i32, [vp, vp, vp, u64, u32, vp, vp, vp]),
             "dsm_generate_text_device": (i32, [vp, ctypes.POINTER(Gen), u64, u64, vp, vp, vp]),
+            # ABI 5: per-system aggregates and the multi-GPU group (RCCL)
+            "dsm_aggregate_device": (i32, [vp, vp, u64, u64, vp, vp]),
+            "dsm_aggregate_results": (i32, [vp, u64, u64, vp]),
+            "dsm_result_digest": (u64, [u64, vp]),
+            "dsm_group_unique_id": (i32, [vp]),
+            "dsm_group_init_rank": (i32, [i32, i32, i32, vp, ctypes.POINTER(vp)]),
+            "dsm_group_init_all": (i32, [i32, vp, vp]),
+            "dsm_group_info": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+            "dsm_group_close": (i32, [vp]),
+            "dsm_group_allreduce": (i32, [vp, vp, ctypes.c_size_t, i32, vp]),
+            "dsm_group_allreduce_counters": (i32, [vp, vp, vp]),
+            "dsm_group_allreduce_aggregate": (i32, [vp, vp, vp]),
+            "dsm_group_barrier": (i32, [vp, vp]),
         }
         for name, (res, args) in sig.items():
             if os.environ.get("DSM_LIB") and not hasattr(L, name):
@@ -152,6 +165,99 @@ def _check(rc, what):
 
 def _ptr(a):
     return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+COUNTERS_BYTES = NCOUNTERS * 8
+NAGG = 16                                    # DSM_NAGG (ABI 5)
+AGG_FIELDS = ("systems", "msgs", "instrs", "rounds", "max_rounds", "st0", "st1", "st2", "st3",
+              "st4", "sum_dump_hash", "sum_final_hash", "result_digest", "reserved0",
+              "reserved1", "reserved2")
+assert len(AGG_FIELDS) == NAGG
+RED_SUM, RED_MAX = 0, 1
+
+
+def _dptr(x, min_bytes=0):
+    """A device pointer argument: an int (raw pointer, unchecked), None, or a tensor, whose
+    size is checked against min_bytes (a dsm_counters buffer of an older ABI is too small)."""
+    if x is None:
+        return None
+    if hasattr(x, "data_ptr"):
+        nb = x.numel() * x.element_size()
+        if nb < min_bytes:
+            raise DsmError(-1, f"device buffer of {nb} bytes, needs {min_bytes}")
+        return ctypes.c_void_p(x.data_ptr())
+    return ctypes.c_void_p(x)
+
+
+def agg_vec_to_dict(v):
+    """A dsm_aggregate (DSM_NAGG uint64) as the golden-aggregate dict (tests/golden/aggregates.json)."""
+    v = [int(x) for x in np.asarray(v, dtype=np.uint64).reshape(-1)]
+    a = dict(zip(AGG_FIELDS, v))
+    out = {k: a[k] for k in ("systems", "msgs", "instrs", "rounds", "max_rounds")}
+    out["status"] = [a[f"st{i}"] for i in range(5)]
+    out.update({k: "0x%016x" % a[k] for k in ("sum_dump_hash", "sum_final_hash", "result_digest")})
+    return out
+
+
+def aggregate_results_c(res, first_idx=0):
+    """dsm_aggregate_results (the library's host fold) of per-system results, as a dict."""
+    res = np.ascontiguousarray(res).view(RESULT_DTYPE).reshape(-1)
+    out = np.zeros(NAGG, dtype=np.uint64)
+    _check(lib().dsm_aggregate_results(_ptr(res), len(res), first_idx, _ptr(out)),
+           "dsm_aggregate_results")
+    return agg_vec_to_dict(out)
+
+
+class Group:
+    """dsm_group: one RCCL communicator per GPU for the end-of-run all-reduces (ABI 5).
+    Rank 0 makes the id (Group.unique_id()) and hands it to every rank out of band."""
+
+    @staticmethod
+    def unique_id():
+        b = (ctypes.c_ubyte * 128)()
+        _check(lib().dsm_group_unique_id(b), "dsm_group_unique_id")
+        return bytes(b)
+
+    def __init__(self, device, nranks, rank, uid):
+        assert len(uid) == 128
+        self.g = ctypes.c_void_p()
+        b = (ctypes.c_ubyte * 128).from_buffer_copy(uid)
+        _check(lib().dsm_group_init_rank(device, nranks, rank, b, ctypes.byref(self.g)),
+               "dsm_group_init_rank")
+
+    def info(self):
+        r, n, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().dsm_group_info(self.g, ctypes.byref(r), ctypes.byref(n), ctypes.byref(d)),
+               "dsm_group_info")
+        return r.value, n.value, d.value
+
+    def allreduce(self, d_buf, n, op=RED_SUM, stream=0):
+        _check(lib().dsm_group_allreduce(self.g, _dptr(d_buf, 8 * n), n, op, ctypes.c_void_p(stream)),
+               "dsm_group_allreduce")
+
+    def allreduce_counters(self, d_counters, stream=0):
+        _check(lib().dsm_group_allreduce_counters(self.g, _dptr(d_counters, COUNTERS_BYTES),
+                                                  ctypes.c_void_p(stream)),
+               "dsm_group_allreduce_counters")
+
+    def allreduce_aggregate(self, d_agg, stream=0):
+        _check(lib().dsm_group_allreduce_aggregate(self.g, _dptr(d_agg, NAGG * 8),
+                                                   ctypes.c_void_p(stream)),
+               "dsm_group_allreduce_aggregate")
+
+    def barrier(self, stream=0):
+        _check(lib().dsm_group_barrier(self.g, ctypes.c_void_p(stream)), "dsm_group_barrier")
+
+    def close(self):
+        if self.g:
+            lib().dsm_group_close(self.g)
+            self.g = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def counters_to_dict(c):
@@ -225,18 +331,23 @@ class Engine:
                                          ctypes.c_void_p(stream)), "dsm_generate_device")
 
     def run_packed_device(self, d_traces, d_counts, n_sys, d_results, d_counters, stream=0):
-        _check(lib().dsm_run_packed_device(self.ctx, ctypes.c_void_p(d_traces),
-                                           ctypes.c_void_p(d_counts), n_sys,
-                                           ctypes.c_void_p(d_results), ctypes.c_void_p(d_counters),
+        """Device pointers (ints) or tensors; a counters tensor must hold DSM_NCOUNTERS slots."""
+        _check(lib().dsm_run_packed_device(self.ctx, _dptr(d_traces), _dptr(d_counts), n_sys,
+                                           _dptr(d_results), _dptr(d_counters, COUNTERS_BYTES),
                                            ctypes.c_void_p(stream)), "dsm_run_packed_device")
 
     def run_generated_device(self, dist, seed, n_instr, first_sys, n_sys, d_results, d_counters,
                              stream=0):
         g = Gen(seed, DIST.get(dist, dist), n_instr)
         _check(lib().dsm_run_generated_device(self.ctx, ctypes.byref(g), first_sys, n_sys,
-                                              ctypes.c_void_p(d_results),
-                                              ctypes.c_void_p(d_counters),
+                                              _dptr(d_results), _dptr(d_counters, COUNTERS_BYTES),
                                               ctypes.c_void_p(stream)), "dsm_run_generated_device")
+
+    def aggregate_device(self, d_results, n_sys, first_sys, d_agg, stream=0):
+        """dsm_aggregate_device: per-system results -> d_agg (DSM_NAGG uint64, accumulated)."""
+        _check(lib().dsm_aggregate_device(self.ctx, _dptr(d_results), n_sys, first_sys,
+                                          _dptr(d_agg, NAGG * 8), ctypes.c_void_p(stream)),
+               "dsm_aggregate_device")
 
     def node_state(self, sys, node):
         d = np.zeros(64, dtype=np.uint8)

@@ -21,8 +21,11 @@
  *
  * Conventions: plain C types only; every function returns 0 (DSM_OK) or a negative DSM_E_*
  * code (dsm_strerror); nothing throws across the ABI.  A dsm_ctx owns its device memory, is
- * bound to one GPU and must be used from one host thread at a time (not reentrant).  The
- * engine runs on hand-written gfx950 HIP kernels only: there is no CPU fallback, and when the
+ * bound to one GPU and must be used from one host thread at a time (not reentrant).  Its
+ * device-side scratch (claim counters, suspended lists, the parser's EXACT-pass file list) is
+ * shared by every call on it, so a ctx runs ONE asynchronous run or parse at a time, on one
+ * stream: enqueue calls on the same ctx onto the same stream (stream order serialises them),
+ * or use one ctx per concurrent stream.  The engine runs on hand-written gfx950 HIP kernels only: there is no CPU fallback, and when the
  * device cannot be used the run functions fail with DSM_E_DEVICE.
  */
 #ifndef DSM_H
@@ -35,9 +38,11 @@
 extern "C" {
 #endif
 
-#define DSM_ABI_VERSION 4   /* 3: dsm_launch_info grew resume_form / budget_rounds / ff_picked;
+#define DSM_ABI_VERSION 5   /* 3: dsm_launch_info grew resume_form / budget_rounds / ff_picked;
                              4: dsm_counters grew to DSM_NCOUNTERS (ser_macro_steps), dsm_launch_info
-                                names the kernels that ran (dsm_launch_kernel_names) */
+                                names the kernels that ran (dsm_launch_kernel_names);
+                             5: per-system aggregates (dsm_aggregate_*) and the multi-GPU group
+                                over RCCL (dsm_group_*) */
 
 #define DSM_MAX_NP 8             /* bitVector is one byte (README.md:51)                  */
 #define DSM_CACHE_SIZE 4         /* CACHE_SIZE      assignment.c:10                        */
@@ -221,8 +226,9 @@ int dsm_run_packed(dsm_ctx *ctx, const uint16_t *traces, const uint32_t *counts,
                    uint64_t n_sys, dsm_sys_result *per_sys, dsm_counters *out);
 
 /* Device buffers (e.g. torch-owned HBM), asynchronous on `stream` (hipStream_t; NULL =
- * null stream).  d_results may be NULL; d_counters (device, one dsm_counters) is
- * ACCUMULATED into.  No host synchronisation inside: every launch (including the two-pass
+ * null stream).  d_results may be NULL; d_counters (device, one dsm_counters: DSM_NCOUNTERS
+ * x uint64 = 320 bytes at ABI 4 -- a 32-slot buffer of ABI 3 is too small and would be written
+ * past its end) is ACCUMULATED into.  No host synchronisation inside: every launch (including the two-pass
  * schedule's resume pass, which sizes itself on the device) is enqueued on `stream`.
  * Device traces are not validated: a count above max_instr is clamped to max_instr, and an
  * instruction whose home node (address >> 4) is >= np ends its system with
@@ -311,7 +317,9 @@ int dsm_set_fast_forward(dsm_ctx *ctx, int mode);
  * with "RD %hhx" / "WR %hhx %hhu" -- into d_traces[f * max_instr ..] (packed u16),
  * d_counts[f] = instructions (at most cap <= max_instr) and d_status[f] (may be NULL) = 0 or
  * the error at the first failing chunk, which also ends the count there: DSM_E_FORMAT (not
- * RD/WR, or a conversion failed) or DSM_E_RANGE (home node >= np).  Asynchronous. */
+ * RD/WR, or a conversion failed) or DSM_E_RANGE (home node >= np).  Asynchronous on `stream`;
+ * it uses the ctx's device file list, so no other run or parse of the same ctx may be in
+ * flight on another stream (see Conventions above). */
 int dsm_parse_traces_device(dsm_ctx *ctx, const char *d_text, const uint64_t *d_offsets,
                             uint64_t n_files, uint32_t cap, uint16_t *d_traces,
                             uint32_t *d_counts, int32_t *d_status, void *stream);
@@ -337,6 +345,67 @@ int dsm_format_run_dumps_device(dsm_ctx *ctx, int view, uint64_t first_sys, uint
 /* GPU-format the dump records of system `sys` of the last run (needs DSM_F_SNAPSHOTS) and
  * write core_<n>_output.txt (:831) for every node n in node_mask into `dir` (NULL = CWD). */
 int dsm_write_run_dumps(dsm_ctx *ctx, uint64_t sys, uint32_t node_mask, const char *dir);
+
+/* ---- per-system aggregates (the shardable result of a run) ---------------------------- *
+ * A run's per-system results folded into the reference's golden-aggregate view
+ * (tests/golden/aggregates.json): sums over systems (mod 2^64), status counts, the max of
+ * rounds, and a position-sensitive result digest -- the sum over systems of a fmix64 chain
+ * over the system's ABSOLUTE id and its six result fields -- so the aggregates of the shards
+ * of an ensemble (GPU g simulates ids [g*n, (g+1)*n)) merge into the job's by
+ * addition, and a max for max_rounds.  DSM_NAGG x uint64, all-reducible as one vector. */
+#define DSM_NAGG 16
+#define DSM_AGG_MAX_SLOT 4       /* the one slot reduced by max (max_rounds)                  */
+typedef struct dsm_aggregate {
+    uint64_t systems;
+    uint64_t msgs;             /* messages handled (transactions)                            */
+    uint64_t instrs;
+    uint64_t rounds;
+    uint64_t max_rounds;       /* max, not sum                                               */
+    uint64_t by_status[5];     /* DSM_COMPLETED .. DSM_ROUND_LIMIT                           */
+    uint64_t sum_dump_hash;
+    uint64_t sum_final_hash;
+    uint64_t result_digest;
+    uint64_t reserved[3];      /* zero (callers may carry their own sums here)               */
+} dsm_aggregate;
+/* d_results[0 .. n_sys) of the systems with ids first_sys, first_sys + 1, .. ACCUMULATED
+ * into d_agg (device; zero it first for one run).  Asynchronous on `stream`. */
+int dsm_aggregate_device(dsm_ctx *ctx, const dsm_sys_result *d_results, uint64_t n_sys,
+                         uint64_t first_sys, dsm_aggregate *d_agg, void *stream);
+/* the same on the host (no GPU needed); agg is overwritten */
+int dsm_aggregate_results(const dsm_sys_result *res, uint64_t n_sys, uint64_t first_sys,
+                          dsm_aggregate *agg);
+/* one system's term of result_digest */
+uint64_t dsm_result_digest(uint64_t sys_id, const dsm_sys_result *r);
+
+/* ---- multi-GPU group: RCCL over xGMI --------------------------------------- *
+ * Systems are independent, so an ensemble shards over GPUs with no data-path exchange; the
+ * only collective is the final all-reduce of the counters and the aggregate (a few hundred
+ * bytes).  A group is one RCCL communicator per GPU, created either
+ *   - by one process per GPU: rank 0 calls dsm_group_unique_id and hands the id to every
+ *     rank by any out-of-band channel, then each calls dsm_group_init_rank; or
+ *   - by one process driving all GPUs (one host thread per device, as the reference runs
+ *     one OpenMP thread per node): dsm_group_init_all, then each thread uses its own group.
+ * The reductions run on the caller's stream (hipStream_t of the group's device), device
+ * buffers in place, and return without a host wait.  Reference: there is no multi-GPU
+ * equivalent in assignment.c; its only sharing is sendMessage's per-node queues (:711-739). */
+#define DSM_GROUP_ID_BYTES 128
+typedef struct dsm_group dsm_group;
+enum { DSM_RED_SUM = 0, DSM_RED_MAX = 1 };
+int dsm_group_unique_id(unsigned char id[DSM_GROUP_ID_BYTES]);
+int dsm_group_init_rank(int device, int nranks, int rank, const unsigned char id[DSM_GROUP_ID_BYTES],
+                        dsm_group **group);
+int dsm_group_init_all(int ndev, const int *devices, dsm_group **groups /* [ndev] */);
+int dsm_group_info(const dsm_group *group, int *rank, int *nranks, int *device);
+int dsm_group_close(dsm_group *group);
+/* n uint64 (mod 2^64 for DSM_RED_SUM) in place */
+int dsm_group_allreduce(dsm_group *group, uint64_t *d_buf, size_t n, int op, void *stream);
+/* dsm_counters in place: every slot summed except max_rounds (max) */
+int dsm_group_allreduce_counters(dsm_group *group, dsm_counters *d_counters, void *stream);
+/* dsm_aggregate in place: every slot summed except max_rounds (max) */
+int dsm_group_allreduce_aggregate(dsm_group *group, dsm_aggregate *d_agg, void *stream);
+/* returns once every rank's `stream` has reached this call (a one-element all-reduce, then
+ * a wait for it on the host) */
+int dsm_group_barrier(dsm_group *group, void *stream);
 
 /* ---- boundary helpers (host only; no GPU needed) ----------------------------------- */
 /* initializeProcessor's parser (:802-818): 20-byte fgets chunks, "RD %hhx" / "WR %hhx %hhu"

@@ -37,6 +37,8 @@ outputs.  Nothing written here is reference source text.
                                                every field in its valid range; record k is
                                                node k % 8)
   tests/golden/aggregates.json                 full-size aggregates of the bench workloads
+                                               (python oracle/gen_fixtures.py aggregates shards
+                                               types shards: + msgs_by_type per entry)
                                                (C3 1M uniform, C4 1M hot, C5 2M evict, and
                                                the 4096-system np8 fixtures): counters,
                                                status counts, hash sums and the per-system
@@ -238,7 +240,35 @@ def merge_aggregates(parts):
         for k in h:
             h[k] = (h[k] + int(p[k], 16)) & M64
     out.update({k: "0x%016x" % v for k, v in h.items()})
+    if all("msgs_by_type" in p for p in parts):
+        out["msgs_by_type"] = [sum(x) for x in zip(*(p["msgs_by_type"] for p in parts))]
     return out
+
+
+def types():
+    """Handled messages per transactionType (assignment.c:20-34) of every reference
+    aggregate entry (ref_lockstep agg's msgs_by_type), added to the entries that lack them;
+    the re-run must reproduce every other field of the entry.  The 2/4/8-GPU job totals are
+    the shard sums (shards() after this)."""
+    p = os.path.join(GOLD, "aggregates.json")
+    out = json.load(open(p))
+    only = os.environ.get("AGG_ONLY")
+    for key, d in sorted(out.items()):
+        if "@x" in key or "msgs_by_type" in d or (only and key.split("@")[0] not in only.split(",")):
+            continue
+        res = subprocess.run([os.path.join(REFBIN, "ref_lockstep_np8"), "agg", str(d["dist"]),
+                              str(d["seed"]), str(d["n_instr"]), str(d["first_sys"]),
+                              str(d["systems"]), str(os.cpu_count() or 8)],
+                             check=True, capture_output=True, text=True)
+        r = json.loads(res.stdout.strip().splitlines()[-1])
+        for k in ("systems", "msgs", "instrs", "rounds", "max_rounds", "status", "sum_dump_hash",
+                  "sum_final_hash", "result_digest"):
+            assert r[k] == d[k], (key, k, r[k], d[k])
+        assert sum(r["msgs_by_type"]) == d["msgs"], key
+        d["msgs_by_type"] = r["msgs_by_type"]
+        print("  ", key, r["msgs_by_type"], flush=True)
+        with open(p, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
 
 
 def shards():

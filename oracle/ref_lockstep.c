@@ -155,9 +155,14 @@ static uint32_t g_round_limit = DSM_ROUND_LIMIT;
 /* inbox limit: MSG_BUFFER_SIZE (:12), or DSM_REF_INBOX_LIMIT (tests; <= MSG_BUFFER_SIZE) */
 static int g_inbox_limit = MSG_BUFFER_SIZE;
 
+/* handled messages of the last run_system by transactionType (:20-34), for the aggregates'
+ * msgs_by_type */
+static uint64_t g_sys_types[13];
+
 static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
     uint32_t rounds = 0, msgs = 0, instrs = 0, status = ST_COMPLETED;
     g_assert_failed = 0;
+    memset(g_sys_types, 0, sizeof g_sys_types);
     for (uint32_t r = 1;; ++r) {
         int acted = 0;
         nst = 0;
@@ -175,6 +180,7 @@ static void run_system(dsm_res *res, dsm_rec *dump, dsm_rec *fin) {
                 message m = c->ring[c->head];
                 c->head = (c->head + 1) % MSG_BUFFER_SIZE;
                 c->count--;
+                if ((unsigned)m.type < 13u) g_sys_types[m.type]++;
                 handle(t, c, m);
                 acted = 1; msgs++;
             } else if (c->node.waitingForReply > 0) {
@@ -234,9 +240,11 @@ static void write_sys(FILE *f, const dsm_res *res, const dsm_rec *dump, const ds
  * not only the totals) */
 typedef struct {
     uint64_t systems, msgs, instrs, rounds, max_rounds, status[5], dh, fh, digest, ns;
+    uint64_t types[13];
 } agg_t;
 
 static void agg_add(agg_t *a, uint64_t idx, const dsm_res *r) {
+    for (int k = 0; k < 13; ++k) a->types[k] += g_sys_types[k];
     a->systems++;
     a->msgs += r->msgs; a->instrs += r->instrs; a->rounds += r->rounds;
     if (r->rounds > a->max_rounds) a->max_rounds = r->rounds;
@@ -251,6 +259,7 @@ static void agg_merge(agg_t *a, const agg_t *b) {
     if (b->max_rounds > a->max_rounds) a->max_rounds = b->max_rounds;
     for (int i = 0; i < 5; ++i) a->status[i] += b->status[i];
     a->dh += b->dh; a->fh += b->fh; a->digest += b->digest;
+    for (int k = 0; k < 13; ++k) a->types[k] += b->types[k];
 }
 
 int main(int argc, char **argv) {
@@ -419,7 +428,7 @@ int main(int argc, char **argv) {
             printf("{\"systems\": %llu, \"msgs\": %llu, \"instrs\": %llu, \"rounds\": %llu, "
                    "\"max_rounds\": %llu, \"status\": [%llu, %llu, %llu, %llu, %llu], "
                    "\"sum_dump_hash\": \"0x%016llx\", \"sum_final_hash\": \"0x%016llx\", "
-                   "\"result_digest\": \"0x%016llx\"}\n",
+                   "\"result_digest\": \"0x%016llx\", \"msgs_by_type\": [",
                    (unsigned long long)tot.systems, (unsigned long long)tot.msgs,
                    (unsigned long long)tot.instrs, (unsigned long long)tot.rounds,
                    (unsigned long long)tot.max_rounds,
@@ -427,6 +436,9 @@ int main(int argc, char **argv) {
                    (unsigned long long)tot.status[2], (unsigned long long)tot.status[3],
                    (unsigned long long)tot.status[4], (unsigned long long)tot.dh,
                    (unsigned long long)tot.fh, (unsigned long long)tot.digest);
+            for (int k = 0; k < 13; ++k)
+                printf("%s%llu", k ? ", " : "", (unsigned long long)tot.types[k]);
+            printf("]}\n");
         }
         return 0;
     }

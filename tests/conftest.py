@@ -25,8 +25,8 @@ def _build():
     """Build the in-tree libraries if they are missing (hipcc cross-compiles without a GPU)."""
     if not os.path.exists(os.path.join(ORACLE, "liboracle.so")):
         subprocess.run(["make", "-C", ORACLE, "liboracle.so"], check=True, stdout=subprocess.DEVNULL)
-    if not (os.path.exists(os.path.join(PKG, "libdsm.so")) and
-            os.path.exists(os.path.join(PKG, "cache_simulator"))):
+    if not all(os.path.exists(os.path.join(PKG, f)) for f in ("libdsm.so", "cache_simulator",
+                                                                "dsm_ensemble")):
         subprocess.run(["make", "-C", PKG, "-j4"], check=True, stdout=subprocess.DEVNULL)
 
 

@@ -104,12 +104,12 @@ def test_launch_kernel_names(kw, want):
 
 def test_abi_version_and_errors():
     L = pydsm.lib()
-    assert L.dsm_abi_version() == 4
+    assert L.dsm_abi_version() == 5
     # the header, the library and the driver's build() check agree on the ABI version
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     hdr = open(os.path.join(root, "include", "dsm.h")).read()
-    assert re.search(r"#define DSM_ABI_VERSION\s+4\b", hdr)
-    assert "dsm_abi_version() == 4" in open(os.path.join(root, "__graft_entry__.py")).read()
+    assert re.search(r"#define DSM_ABI_VERSION\s+5\b", hdr)
+    assert "dsm_abi_version() == 5" in open(os.path.join(root, "__graft_entry__.py")).read()
     assert pydsm.strerror(0) == "ok"
     for code in range(-7, 0):
         assert pydsm.strerror(code) != "unknown error"

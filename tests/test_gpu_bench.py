@@ -1,7 +1,8 @@
 """GPU: bench.py end to end on the one GPU of the box -- the 1-rank line, `--gpus 2` through
 its own launcher (both ranks on device 0, counters over gloo: RCCL needs a GPU per rank), whose
-whole-job counters must equal one rank simulating both shards, and the RCCL path (process
-group, barriers, all-reduce of the counters and of the elapsed time) at one rank."""
+whole-job counters must equal one rank simulating both shards, the RCCL path (libdsm's
+dsm_group_*: barriers, all-reduce of the counters, the aggregate and the elapsed time) at one
+rank, and the C multi-GPU driver (dsm_ensemble) at one GPU."""
 import json
 import os
 import subprocess
@@ -40,22 +41,37 @@ def test_two_rank_launch_equals_one_rank_over_both_shards():
 
 
 def test_rccl_collective_path_one_rank():
-    """bench.py's torch.distributed path on the nccl backend (RCCL), forced at world size 1:
-    init with device_id, the barriers around the timed region, the MAX all-reduce of the
-    elapsed time and the SUM / MAX all-reduce of the counters -- the same results as the plain
-    run."""
-    import socket
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    env = {"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "LOCAL_WORLD_SIZE": "1",
-           "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "DSM_BENCH_DIST": "1"}
-    rccl = _bench(["--gpus", "1"] + SMALL, env=env)
-    plain = _bench(["--gpus", "1"] + SMALL)
-    assert rccl["collective"].startswith("rccl all_reduce") and plain["collective"] is None
+    """bench.py's default collective path at one rank: libdsm's own RCCL communicator
+    (dsm_group_init_rank over a single-rank id), the RCCL barriers around the timed region,
+    the MAX all-reduce of the elapsed time and the SUM / MAX all-reduces of the counters and of
+    the aggregate (dsm_group_allreduce_*) -- the same results as the run without any
+    collective (the gloo backend at one rank)."""
+    rccl = _bench(["--gpus", "1"] + SMALL)
+    plain = _bench(["--gpus", "1"] + SMALL, env={"DSM_BENCH_BACKEND": "gloo"})
+    assert rccl["collective"].startswith("rccl ncclAllReduce issued by libdsm"), rccl["collective"]
+    assert plain["collective"] is None
     for k in ("msgs", "instrs", "rounds", "systems", "max_rounds", "status_DEADLOCKED"):
         assert rccl["counters"][k] == plain["counters"][k], k
     assert rccl["sum_final_hash"] == plain["sum_final_hash"]
+    # the untimed per-type pass: 13 counts summing to the timed run's messages
+    assert sum(rccl["msgs_by_type"].values()) == rccl["counters"]["msgs"]
+    assert "msgs_by_type" in rccl["parity"] and "MISMATCH" not in rccl["parity"], rccl["parity"]
+
+
+def test_c_driver_one_gpu_pinned_prefix():
+    """bench.py --driver c: the C multi-GPU driver (dsm_ensemble, one host thread per GPU,
+    RCCL through dsm_group_init_all) at one GPU over the 4096 systems the golden per-system
+    fixture pins: its device aggregate (dsm_aggregate_device) and the reduced counters equal the
+    reference's, and its per-type counts sum to the messages."""
+    line = _bench(["--driver", "c", "--gpus", "1", "--systems", "4096", "--steps", "2",
+                   "--warmup", "1"])
+    assert line["n_gpus"] == 1 and line["driver"].startswith("dsm_ensemble (C")
+    assert line["parity"].startswith("full-size aggregate == reference (job total over 1 shard(s), "
+                                     "aggregates.json:np8_uniform)"), line["parity"]
+    assert "1/1 shards" in line["parity"] and "MISMATCH" not in line["parity"]
+    assert "msgs_by_type == reference (13 types)" in line["parity"], line["parity"]
+    assert sum(line["msgs_by_type"].values()) == line["counters"]["msgs"]
+    assert line["value"] > 0 and line["collective"].startswith("rccl ncclAllReduce over 1 GPU")
 
 
 @pytest.mark.parametrize("gpus,config,n", [(2, "random", 2048), (4, "evict", 1024)])

@@ -11,6 +11,6 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$T/include $
 $H -c "$T/csrc/dsm_engine.hip" -o "$T/e.o" 2>"$T/warn.txt" || { cat "$T/warn.txt"; exit 1; }
 grep -i "spill\|occupancy" "$T/warn.txt" | head -5 || true
 mkdir -p ab
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$T/e.o" hp-assignment-2_amd/build/dsm_text.o hp-assignment-2_amd/build/dsm_host.o -o "ab/libdsm_$NAME.so"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$T/e.o" hp-assignment-2_amd/build/dsm_text.o hp-assignment-2_amd/build/dsm_host.o hp-assignment-2_amd/build/dsm_group.o -L/opt/rocm/lib -lrccl -o "ab/libdsm_$NAME.so"
 rm -rf "$T"
 echo "ab/libdsm_$NAME.so"
