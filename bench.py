@@ -800,7 +800,7 @@ def main():
             "counters": {k: c[k] for k in ("msgs", "instrs", "rounds", "systems", "max_rounds",
                                            "overflow_reruns", "wave_rounds", "resumed",
                                            "ff_passes", "ff_steps", "ff_sample_instrs",
-                                           "ff_sample_runs", "ser_macro_steps", "status_COMPLETED",
+                                           "ff_sample_runs", "ser_macro_steps", "ser_iterations", "status_COMPLETED",
                                            "status_DEADLOCKED")},
             "msgs_by_type": dict(zip(pydsm.TYPE_NAMES, type_pass["msgs_by_type"])) if type_pass else None,
             "type_pass": {k: v for k, v in (type_pass or {}).items() if k != "msgs_by_type"} or None,

@@ -84,6 +84,10 @@ struct SimArgs {
     uint32_t *susp;                 /* [sys][word][node] suspended state (susp_words)        */
     uint32_t *susp_list;            /* budget pass: suspended system ids                     */
     unsigned int *susp_count;
+    unsigned int *susp_long;        /* serial-form budget pass: systems of the long class, listed
+                                     * from the list's top down (SER_LONG); the serial pass
+                                     * claims them first                                     */
+    uint32_t susp_cap;              /* the list's capacity (systems in the run)              */
     uint32_t lim_rsh;               /* round limit = 1 << lim_rsh (DSM_MAX_ROUNDS, or
                                      * dsm_set_round_limit): ROUND_LIMIT at that many rounds */
     uint32_t icap;                  /* inbox limit (MSG_BUFFER_SIZE = 256, or
@@ -121,6 +125,11 @@ DEVI void wait_vmcnt0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 #define TRAFFIC_PROBE 0     /* traffic attribution builds (results invalid): 1 no serial pass, 2 and
                                no serial-form suspend records (tools/traffic_streams.sh) */
 #endif
+#ifndef SER_LONG
+#define SER_LONG 0          /* the serial pass claims lone systems with this many instructions left
+                               (and multi-node ones) first, the rest last-suspended first (0: all
+                               last-suspended first) */
+#endif
 #ifndef SIM_TAILPROBE
 #define SIM_TAILPROBE 0     /* budget-pass wave end-time histogram (probe build, results exact;
                                tools/tail_probe.py) */
@@ -150,7 +159,9 @@ constexpr uint32_t C_WAIT = DT_CTL_WAIT, C_DUMPED = 1u << 9, C_OVF = 1u << 10, C
 enum { K_MSGS = 13, K_INSTRS = 14, K_ROUNDS = 15, K_SYSTEMS = 16, K_STATUS = 17, K_DHASH = 22,
        K_FHASH = 23, K_MAXR = 24, K_OVFRERUN = 25, K_WROUNDS = 26, K_RESUMED = 27,
        K_FFPASS = 28, K_FFITER = 29, K_SCANI = 30, K_SCANR = 31, K_N = 32,
-       K_SERMAC = 32 /* ser_kernel only, added straight to the device counters */ };
+       K_SERMAC = 32 /* ser_kernel only, added straight to the device counters */,
+       K_SERIT = 33  /* ser_kernel only: its wave iterations (dsm_counters.ser_iterations)  */,
+       K_SERPROBE = 34 /* SIM_TAILPROBE builds: the serial pass's wave end-time histogram, 34-39 */ };
 static_assert(sizeof(dsm_counters) == DSM_NCOUNTERS * 8 && K_SERMAC < DSM_NCOUNTERS, "dsm_counters slots");
 constexpr uint32_t RSH_MAX = 22;    /* 1 << 22 == DSM_MAX_ROUNDS */
 static_assert((1u << RSH_MAX) == DSM_MAX_ROUNDS, "DSM_MAX_ROUNDS");
@@ -1093,11 +1104,22 @@ sim_kernel(const SimArgs *Ap) {
                         for (int k = 0; k < 4; ++k) { q[(7 + k) * NP] = cur[k]; q[(11 + k) * NP] = nxt[k]; }
                     }
                     const uint32_t ins = gsum32<NP>(nd.ip), msgs = gsum32<NP>(nd.nmsg - (FB ? 0u : nd.rh >> 8));
+                    /* the serial pass's claim order, longest first by class: a lone system whose
+                     * lone node has SER_LONG or more instructions left (the one lane with
+                     * any: a group sum), or one still running several nodes, is long */
+                    uint32_t lrem = 0;
+                    if (SER_LONG && LONE)
+                        lrem = gsum32<NP>((lone && (nd.ctl & (C_WAIT | C_DUMPED)) == 0u) ? nd.nins - nd.ip : 0u);
                     uint32_t nlo = 0xFFFFFFFFu, nhi = 0xFFFFFFFFu;
                     if (node == 0) {
                         if (susp) {
-                            const uint32_t pos = atomicAdd(Ap->susp_count, 1u);
-                            Ap->susp_list[pos] = (uint32_t)sys;
+                            if (SER_LONG && LONE && ser_fmt && (!lone || lrem >= (uint32_t)SER_LONG)) {
+                                const uint32_t lp = atomicAdd(Ap->susp_long, 1u);
+                                Ap->susp_list[Ap->susp_cap - 1u - lp] = (uint32_t)sys;
+                            } else {
+                                const uint32_t pos = atomicAdd(Ap->susp_count, 1u);
+                                Ap->susp_list[pos] = (uint32_t)sys;
+                            }
                             atomicAdd(&s_cnt[wv][K_RESUMED], 1ull);
                         } else if (handoff) {
                             const uint32_t pos = atomicAdd(Ap->ovf_count, 1u);
@@ -1229,7 +1251,7 @@ sim_kernel(const SimArgs *Ap) {
      * depend on the order, so no separate reduction pass is needed) */
     if (lane == 0) {
         s_cnt[wv][K_WROUNDS] = wrounds;
-#if SIM_TAILPROBE
+#if SIM_TAILPROBE == 1
         /* probe build (results exact, not the default): when the budget pass's waves end, a
          * histogram in the msgs_by_type slots -- 0: before 14 ms, k = 1..11: [13 + k, 14 + k)
          * ms, 12: the waves' summed lifetimes in 10-ns ticks (s_memrealtime, 100 MHz) */
@@ -1349,17 +1371,25 @@ ser_kernel(const SimArgs *Ap) {
     if (threadIdx.x < K_N) s_cnt[threadIdx.x] = 0;
     for (uint32_t i = threadIdx.x; i < DT_TABLE_WORDS / 2; i += 64 * SER_WAVES) s_tab[i] = Ap->table[i];
     __syncthreads();
+#if SIM_TAILPROBE
+    const uint64_t tprobe0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     const LdsCol<SER_WAVES> m{s_ser, &s_dum[lane], wv, lane,
                               (GU32 *)(Ap->spill + ((uint64_t)blockIdx.x * (64 * SER_WAVES) + threadIdx.x) * S_SPILL)};
     const LdsTab T{s_tab};
-    const uint32_t n = *Ap->d_n;
-    /* claim k -> system: last-suspended first, as the lock-step resume (whose records are the
-     * likeliest still in the MALL; longest-first orders measured slower) */
+    /* claim k -> system: the long class first (SER_LONG: listed from the top down by the
+     * budget pass, taken in suspension order), then the rest last-suspended first, as the
+     * lock-step resume (their records the likeliest still in the MALL) */
+    const uint32_t nlong = (SER_LONG && Ap->serfmt && Ap->susp_long) ? *Ap->susp_long : 0u;
+    const uint32_t n = *Ap->d_n + nlong;
+    const uint32_t lcap = Ap->susp_cap;
     const uint32_t *const list = Ap->list;
     /* global (not flat) accesses: a pending flat operation makes every later wait a full
      * vmcnt(0) lgkmcnt(0), the LDS waits of the macro-step included */
-    auto sel = [&](uint32_t k) -> uint32_t { return ((const GU32 *)list)[n - 1 - k]; };
+    auto sel = [&](uint32_t k) -> uint32_t {
+        return ((const GU32 *)list)[k < nlong ? lcap - 1u - k : n - 1u - k];
+    };
 
     const uint32_t stride = Ap->stride, lim_rsh = Ap->lim_rsh, SR = Ap->susp_ring;
     const uint32_t cap = Ap->icap;
@@ -1627,6 +1657,13 @@ ser_kernel(const SimArgs *Ap) {
     }
     v = live ? start() : SR_RUN;
     uint32_t iters = 0, nmac = 0;
+#if SIM_TAILPROBE == 2
+    /* probe: per lane, the iteration its system started at and whether it was lone at
+     * suspension (header word 121), and running maxima / sums published at the kernel's end */
+    uint32_t tclaim = 0;
+    bool lone0 = live && serfmt && (rr[30].y & 0x100u);
+    uint64_t pr_long = 0, pr_last = 0, pr_n4k = 0, pr_nl_it = 0, pr_it = 0, pr_nl_n = 0;
+#endif
     /* batched hand-overs: a hand-over is a wave-wide phase (~19k cycles on C3, most of it
      * waits on the claim, the lookup, the successor's rows and the record stores) however
      * few lanes take part, so a finished system waits, its lane idle, until SER_HB lanes of
@@ -1719,6 +1756,9 @@ ser_kernel(const SimArgs *Ap) {
                 hgo = true;
             }
             if (hgo && live && v != SR_RUN) {
+#if SIM_TAILPROBE == 2
+                const uint32_t now_it = iters + (uint32_t)k;   /* this iteration (before the claim's k) */
+#endif
                 uint64_t th0 = 0, th1 = 0, th2 = 0;
                 if (SER_PROBE >= 3) th0 = __builtin_amdgcn_s_memtime();
                 /* the successor: claimed and looked up first (waits that cover nothing but
@@ -1738,6 +1778,21 @@ ser_kernel(const SimArgs *Ap) {
                 const uint32_t ns = nl ? sel(k) : 0u;
                 if (nl && serfmt) load_rec(ns);
                 if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th1 = __builtin_amdgcn_s_memtime(); }
+#if SIM_TAILPROBE == 2
+                {   /* probe: the longest system, and the duration of the system that ends last */
+                    const uint64_t dur = (uint64_t)(now_it - tclaim);
+                    const uint64_t a = (dur << 32) | (uint64_t)sys;
+                    const uint64_t b = ((uint64_t)now_it << 32) | ((uint64_t)lone0 << 31) | dur;
+                    pr_long = a > pr_long ? a : pr_long;
+                    pr_last = b > pr_last ? b : pr_last;
+                    pr_n4k += dur > 4000u ? 1u : 0u;
+                    pr_nl_it += lone0 ? 0u : dur;
+                    pr_it += dur;
+                    pr_nl_n += lone0 ? 0u : 1u;
+                    tclaim = now_it;
+                    lone0 = nl && serfmt && (rr[30].y & 0x100u);
+                }
+#endif
                 finish(v);
                 if (SER_PROBE >= 3) { __builtin_amdgcn_s_waitcnt(0); th2 = __builtin_amdgcn_s_memtime(); }
                 live = nl;
@@ -1768,7 +1823,34 @@ ser_kernel(const SimArgs *Ap) {
         iters += SER_RF;
         if (__ballot(live) == 0) break;
     }
-    if (lane == 0) atomicAdd(&s_cnt[K_WROUNDS], (unsigned long long)iters);
+#if SIM_TAILPROBE == 2
+    {
+        uint64_t v6[6] = {pr_long, pr_last, pr_n4k, pr_nl_it, pr_it, pr_nl_n};
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            uint64_t x = v6[q];
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t lo = __shfl_xor((uint32_t)x, o, 64), hi = __shfl_xor((uint32_t)(x >> 32), o, 64);
+                const uint64_t y = ((uint64_t)hi << 32) | lo;
+                x = q < 2 ? (y > x ? y : x) : x + y;
+            }
+            if (lane == 0) {
+                if (q < 2) atomicMax(&Ap->counters[q], (unsigned long long)x);
+                else atomicAdd(&Ap->counters[q], (unsigned long long)x);
+            }
+        }
+    }
+#endif
+    if (lane == 0) {
+        atomicAdd(&s_cnt[K_WROUNDS], (unsigned long long)iters);
+        atomicAdd(&Ap->counters[K_SERIT], (unsigned long long)iters);
+#if SIM_TAILPROBE
+        /* probe build: when the serial pass's waves end, ms after the wave started -- slot 34:
+         * before 11 ms, 35..38: [10 + k, 11 + k) for k = 1..4, 39: 15 ms and later */
+        const uint64_t ms = (__builtin_amdgcn_s_memrealtime() - tprobe0) / 100000u;
+        atomicAdd(&Ap->counters[K_SERPROBE + (ms < 11u ? 0u : (ms - 10u < 5u ? ms - 10u : 5u))], 1ull);
+#endif
+    }
     if (!CAP) {          /* lone-node transaction steps (ser_macro): one atomic per wave */
         uint32_t t = nmac;
         for (int o = 1; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
@@ -2022,7 +2104,8 @@ static_assert(sizeof(SimArgsPack) % 4 == 0, "SimArgsPack words");
 #define CTRL_FB 256
 #define CTRL_OVF 512
 #define CTRL_RES 1024       /* claim shards of the resume pass */
-#define CTRL_SUSP 1536      /* systems the budget pass suspended */
+#define CTRL_SUSP 1536      /* systems the budget pass suspended (the short class with SER_LONG) */
+#define CTRL_SUSPL 1568     /* ... of the long class (SER_LONG), listed from the top down */
 #define CTRL_SCAN 1792      /* ffscan_kernel's sample counts */
 
 /* Two-pass schedule (bench mode: MODE 0, packed traces).  A system's length is unknown until
@@ -2184,6 +2267,7 @@ static const char *build_variant() {
         if (v != def && n < (int)sizeof tag) n += snprintf(tag + n, sizeof tag - n, " %s=%ld", name, v);
     };
     add("SIM_BF", SIM_BF, 0);
+    add("SER_LONG", SER_LONG, 0);
     add("SIM_TAILPROBE", SIM_TAILPROBE, 0);
     add("TRAFFIC_PROBE", TRAFFIC_PROBE, 0);
     add("SER_PROBE", SER_PROBE, 0);
@@ -2372,6 +2456,8 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     A.susp = c->d_susp;
     A.susp_list = c->d_susp_list;
     A.susp_count = c->d_ctrl + CTRL_SUSP;
+    A.susp_long = c->d_ctrl + CTRL_SUSPL;
+    A.susp_cap = (uint32_t)n_sys;
     A.susp_ring = (uint32_t)ring_eff;
     A.spill = c->d_spill;
     if (tr) {

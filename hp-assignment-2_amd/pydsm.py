@@ -33,9 +33,9 @@ COUNTER_FIELDS = ([f"msgs_{t}" for t in TYPE_NAMES] +
                   [f"status_{s}" for s in STATUS_NAMES] +
                   ["sum_dump_hash", "sum_final_hash", "max_rounds", "overflow_reruns",
                    "wave_rounds", "resumed", "ff_passes", "ff_steps", "ff_sample_instrs",
-                   "ff_sample_runs", "ser_macro_steps"] +
-                  [f"reserved_{i}" for i in range(7)])
-NCOUNTERS = 40                               # DSM_NCOUNTERS (ABI 4)
+                   "ff_sample_runs", "ser_macro_steps", "ser_iterations"] +
+                  [f"reserved_{i}" for i in range(6)])
+NCOUNTERS = 40                               # DSM_NCOUNTERS (ABI 4; ser_iterations: ABI 5)
 assert len(COUNTER_FIELDS) == NCOUNTERS
 MAX_SLOT = COUNTER_FIELDS.index("max_rounds")   # the one counter that is a max, not a sum
 

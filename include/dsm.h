@@ -163,7 +163,9 @@ typedef struct dsm_counters {
     uint64_t ff_sample_runs;   /* ... of them ending a run of 8 hits (a private 4-line model) */
     uint64_t ser_macro_steps;  /* ABI 4: lone-node whole-transaction steps of the serial resume
                                 * pass (dsm_serial.h ser_macro)                              */
-    uint64_t reserved[7];      /* zero                                                       */
+    uint64_t ser_iterations;   /* ABI 5: wave iterations of the serial resume pass (cost model;
+                                * wave_rounds holds them too, with the lock-step rounds)      */
+    uint64_t reserved[6];      /* zero (probe builds: diagnostics)                            */
 } dsm_counters;
 
 typedef struct dsm_ctx dsm_ctx;

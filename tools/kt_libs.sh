@@ -4,6 +4,7 @@
 # gpurun_out/kt_libs/<build>_<dist>/ (kt_kernel_stats.csv), to split an A/B by kernel
 D=$1; N=$2; shift 2
 cd /tmp && export TMPDIR=/tmp; cd - >/dev/null
+mkdir -p gpurun_out/kt_libs
 for L in "$@"; do
   B=$(basename "$L" .so)
   export DSM_LIB=$L
