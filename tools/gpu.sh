@@ -32,10 +32,10 @@ for s in "$@"; do
                  --timeout-method thread ${a:+-k "$a"} ;;
     bench)   if [ "$b" = cpu ]; then step "bench_${a}_cpu" 600 python -u bench.py --config "$a"
              else step "bench_$a" 400 python -u bench.py --config "$a" --no-cpu; fi ;;
-    profile) bash tools/profile.sh "$a" --config "$b" --steps 3 --warmup 1 || exit $? ;;
+    profile) bash tools/profile.sh "$a" --config "$b" --steps 3 --warmup 1 --no-types || exit $? ;;
     kt)      mkdir -p "gpurun_out/prof_$a"
              step "kt_$a" 600 rocprofv3 --kernel-trace --stats --output-format csv \
-                 -d "gpurun_out/prof_$a/kt" -o kt -- python3 bench.py --no-cpu --config "$b" \
+                 -d "gpurun_out/prof_$a/kt" -o kt -- python3 bench.py --no-cpu --no-types --config "$b" \
                  --steps 3 --warmup 1 ;;
     ab)      step "ab_${a}_${e:-uniform}" 600 python -u tools/ab_open.py "$a" "$b" "${c:-1048576}" "${d:-2}" "${e:-uniform}" ;;
     abl)     step "abl_${a}" 600 bash tools/ab_libs.sh "$a" "$b" ${c//,/ } ;;
