@@ -125,6 +125,14 @@ DEVI void wait_vmcnt0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 #define TRAFFIC_PROBE 0     /* traffic attribution builds (results invalid): 1 no serial pass, 2 and
                                no serial-form suspend records (tools/traffic_streams.sh) */
 #endif
+#ifndef SIM_UNI
+#define SIM_UNI 1           /* the suspend-on-lone budget pass's per-round end test as one per-lane
+                               ballot, not 64-bit mask arithmetic (0: the mask form everywhere) */
+#endif
+#ifndef REC_PROBE
+#define REC_PROBE 0         /* probe build (hashes invalid): no node records and no digest pass, to
+                               time what the records cost the step */
+#endif
 #ifndef SER_LONG
 #define SER_LONG 0          /* the serial pass claims lone systems with this many instructions left
                                (and multi-node ones) first, the rest last-suspended first (0: all
@@ -459,6 +467,7 @@ sim_kernel(const SimArgs *Ap) {
     /* suspend-on-lone and the serial-form record: the plain budget kernel of a serial-resumed
      * run only (M_SERB) */
     constexpr bool LONE = BUD && !FF && (MODE & M_SERB) != 0;
+    constexpr bool UNI = SIM_UNI != 0 && LONE;     /* the per-round end test as one ballot */
     constexpr int SW = susp_words(RING);
     /* fast-forward probe interval: FF_PROBE iterations after a probe that found a group,
      * doubling up to FF_PROBE_MAX after each one that found none (workloads without hit
@@ -939,7 +948,7 @@ sim_kernel(const SimArgs *Ap) {
             }
             if (doDump) {                                                    /* :688-697 */
                 nd.ctl |= C_DUMPED;               /* printProcessorState(threadId, node), :695 */
-                store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8, nd, s_mb, s_line, wv, lane, 2u);
+                if (!REC_PROBE) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8, nd, s_mb, s_line, wv, lane, 2u);
             }
 
             /* ---- (4) end-of-round delivery: ascending sender, then program order --------- */
@@ -1022,12 +1031,26 @@ sim_kernel(const SimArgs *Ap) {
                 loneb = lone_mask();
             }
             /* rounds >= thr: the round limit, or the budget pass's budget */
-            const uint64_t flagb = __ballot((nd.ctl & C_ASSERT) != 0u || rounds >= thr) |
-                                   __ballot(nccv > ocap) | loneb;
-            constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
-            constexpr uint64_t GHI = GLO << (NP - 1);
-            const uint64_t t = actb | ~liveb;
-            if ((((t - GLO) & ~t & GHI) | (flagb & liveb)) == 0) return;
+            if constexpr (UNI) {
+                /* one ballot: a live lane whose group has no active lane (its field of actb), or
+                 * with an assert, the round limit / budget or an overflowing inbox (C3 budget
+                 * pass 24.5 -> 23.8 ms, C5 15.9 -> 15.5; in the kernel without suspend-on-lone,
+                 * C4's, 17.3 -> 17.6: there the mask form below is kept) */
+                const uint32_t gidle = ((uint32_t)(actb >> gbase) & NPM) == 0u;
+                /* bitwise, not && / ||: short-circuit conditions are compiled into branches */
+                const uint32_t endc = (uint32_t)live & (gidle | (uint32_t)((nd.ctl & C_ASSERT) != 0u) |
+                                                        (uint32_t)(rounds >= thr) | (uint32_t)(nccv > ocap));
+                const uint64_t endb = __ballot(endc != 0u) | loneb;
+                if (endb == 0) return;
+            } else {
+                /* a group field of actb | ~liveb that is zero: a live group with no active lane */
+                const uint64_t flagb = __ballot((nd.ctl & C_ASSERT) != 0u || rounds >= thr) |
+                                       __ballot(nccv > ocap) | loneb;
+                constexpr uint64_t GLO = NP == 8 ? 0x0101010101010101ull : 0x1111111111111111ull;
+                constexpr uint64_t GHI = GLO << (NP - 1);
+                const uint64_t t = actb | ~liveb;
+                if ((((t - GLO) & ~t & GHI) | (flagb & liveb)) == 0) return;
+            }
             if (nccv > ocap) nd.ctl |= C_OVF;
             const uint32_t gact = (uint32_t)(actb >> gbase) & NPM;
             const uint64_t badb = __ballot(live && (nd.ctl & (C_ASSERT | C_OVF)));
@@ -1053,7 +1076,7 @@ sim_kernel(const SimArgs *Ap) {
                     else st = DSM_ROUND_LIMIT;
                     const bool handoff = !FB && (st == DSM_RING_OVERFLOW);
                     const uint32_t fl = ((nd.ctl & C_WAIT) ? 1u : 0u) | ((nd.ctl & C_DUMPED) ? 2u : 0u);
-                    if (!handoff && !susp) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
+                    if (!handoff && !susp && !REC_PROBE) store_rec<WAVES>(Ap->recs + (sys * NP + node) * 8 + 4, nd, s_mb, s_line, wv, lane, fl);
                     if (susp && ser_fmt && TRAFFIC_PROBE < 2) {    /* the serial pass's record (ssusp_words) */
                         uint32_t *sp = Ap->susp + sys * (uint64_t)ssusp_words(RING);
                         uint4 *mb = reinterpret_cast<uint4 *>(sp + 8u * node);     /* S_MB + 8 n */
@@ -1542,6 +1565,7 @@ ser_kernel(const SimArgs *Ap) {
         return SR_RUN;
     };
     auto store_rec = [&](uint32_t nd, uint32_t flags, uint32_t which) {
+        if (REC_PROBE) return;
         GV4 *dst = (GV4 *)(recs + (sys * NP + nd) * 8 + 4u * which);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -2268,6 +2292,8 @@ static const char *build_variant() {
     };
     add("SIM_BF", SIM_BF, 0);
     add("SER_LONG", SER_LONG, 0);
+    add("REC_PROBE", REC_PROBE, 0);
+    add("SIM_UNI", SIM_UNI, 1);
     add("SIM_TAILPROBE", SIM_TAILPROBE, 0);
     add("TRAFFIC_PROBE", TRAFFIC_PROBE, 0);
     add("SER_PROBE", SER_PROBE, 0);
@@ -2541,7 +2567,8 @@ static int run_engine(dsm_ctx *c, bool gen, const dsm_gen *g, uint64_t first_sys
     HIPCK(hipGetLastError());
 
     unsigned long long *dcnt = reinterpret_cast<unsigned long long *>(d_counters);
-    if (np == 4)
+    if (REC_PROBE) {}
+    else if (np == 4)
         hipLaunchKernelGGL(digest_kernel<4>, dim3((unsigned)dblocks), dim3(256), 0, st, n_sys,
                            (const uint4 *)c->d_recs, d_results, dcnt);
     else
