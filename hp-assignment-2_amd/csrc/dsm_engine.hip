@@ -2200,9 +2200,11 @@ extern "C" int dsm_open(int device, const dsm_config *cfg, dsm_ctx **out) {
     c->inbox_limit = FB_RING;
     c->ff_mode = DSM_FF_AUTO;
     c->serial = (int)env_u32("DSM_SERIAL", 1);
-    /* the budget pass checks for quiet-lone systems every DSM_LONE rounds (0: never) */
+    /* the budget pass checks for quiet-lone systems every DSM_LONE rounds (0: never), from
+     * round DSM_LONE_MIN on (160, round 6: C5 29.4 -> 28.5 ms, C3 within its spread; 128 costs
+     * C3 +0.4, 96 and below cost C5 3+ ms: too many multi-node systems reach the serial pass) */
     c->lone_rounds = env_u32("DSM_LONE", 8);
-    c->lone_min = env_u32("DSM_LONE_MIN", 256);
+    c->lone_min = env_u32("DSM_LONE_MIN", 160);
 
     c->fmt_tile = (int)env_u32("DSM_FMT", 132);
     c->parse_bpl = (int)env_u32("DSM_PARSE_BPL", 32);
