@@ -120,6 +120,10 @@ struct SimArgsPack { SimArgs a[3]; };
 #error "dsm_engine.hip targets gfx950 (raw gfx9 s_waitcnt encodings)"
 #endif
 DEVI void wait_vmcnt0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+/* a wave-uniform value stated as such (v_readfirstlane): branches on it compile to scalar
+ * branches, not exec-masked regions, whatever the compiler's uniformity analysis concluded */
+DEVI uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+DEVI uint64_t uni64(uint64_t x) { return ((uint64_t)uni32((uint32_t)(x >> 32)) << 32) | uni32((uint32_t)x); }
 
 #ifndef TRAFFIC_PROBE
 #define TRAFFIC_PROBE 0     /* traffic attribution builds (results invalid): 1 no serial pass, 2 and
@@ -128,6 +132,10 @@ DEVI void wait_vmcnt0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 #ifndef SIM_UNI
 #define SIM_UNI 1           /* the suspend-on-lone budget pass's per-round end test as one per-lane
                                ballot, not 64-bit mask arithmetic (0: the mask form everywhere) */
+#endif
+#ifndef SIM_RFL
+#define SIM_RFL 1           /* the round loop's wave-uniform values (the live mask, the end test,
+                               the lone-check countdown) pinned uniform with readfirstlane */
 #endif
 #ifndef REC_PROBE
 #define REC_PROBE 0         /* probe build (hashes invalid): no node records and no digest pass, to
@@ -502,7 +510,12 @@ sim_kernel(const SimArgs *Ap) {
     const uint64_t tprobe0 = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    const uint64_t n = Ap->d_n ? (uint64_t)*Ap->d_n : Ap->n_sys;
+    /* values read through loaded (generic) pointers count as lane-varying to the compiler's
+     * uniformity analysis, which then takes every branch that depends on them -- the round
+     * loop's -- as divergent: SIM_RFL states them uniform */
+    const uint64_t n = SIM_RFL ? uni64(Ap->d_n ? (uint64_t)*Ap->d_n : Ap->n_sys)
+                               : (Ap->d_n ? (uint64_t)*Ap->d_n : Ap->n_sys);
+    const bool ffv = SIM_RFL ? uni32(ff_verdict(Ap->scan)) != 0u : ff_verdict(Ap->scan);
     const uint32_t *list = Ap->list;
     const uint64_t G = ((uint64_t)blockIdx.x * WAVES + wv) * GPW + lane / NP;
     uint32_t shard = blockIdx.x & 7u, tried = 0;
@@ -518,17 +531,17 @@ sim_kernel(const SimArgs *Ap) {
     const uint32_t rsh0 = BUD && Ap->rsh < lim_rsh ? Ap->rsh : lim_rsh;
     /* the round test's threshold: the round limit, or the budget pass's budget (wave-uniform) */
     uint32_t thr = 1u << rsh0;
-    if (BUD && Ap->budget && Ap->thr_ff && (FF || (Ap->ffsel && ff_verdict(Ap->scan))) &&
+    if (BUD && Ap->budget && Ap->thr_ff && (FF || (Ap->ffsel && ffv)) &&
         Ap->thr_ff < (1u << lim_rsh))
         thr = Ap->thr_ff;          /* a fast-forward workload's budget (thr_ff, run_engine) */
     const uint32_t late_rsh = BUD ? Ap->late_rsh : 0u;
     const bool budget = BUD && Ap->budget != 0, resume = BUD && Ap->resume != 0;
     /* suspend-on-lone: the budget pass of a run whose resume pass is the serial one (not the
      * fast-forward pair's pick) */
-    const uint32_t lone_on = (LONE && budget && !(Ap->ffsel && ff_verdict(Ap->scan))) ? Ap->lone : 0u;
+    const uint32_t lone_on = (LONE && budget && !(Ap->ffsel && ffv)) ? Ap->lone : 0u;
     uint32_t lcd = lone_on;             /* rounds to the next check (uniform) */
     const uint32_t lone_min = Ap->lone_min;   /* not before this many rounds */
-    const bool ser_fmt = LONE && budget && Ap->serfmt && !(Ap->ffsel && ff_verdict(Ap->scan));
+    const bool ser_fmt = LONE && budget && Ap->serfmt && !(Ap->ffsel && ffv);
     /* systems started statically (one per slot), the rest claimed from the shard counters.
      * The resume pass is launched at the full grid and sizes itself here from the device-
      * resident count of suspended systems (no host round trip): it uses the fewest slots
@@ -1026,6 +1039,7 @@ sim_kernel(const SimArgs *Ap) {
             asm volatile("" : "+v"(opv));
             const uint64_t actb = __ballot(opv != OP_IDLE || stall) | (WFF ? ffm : 0ull);
             uint64_t loneb = 0;
+            if (SIM_RFL) lcd = uni32(lcd);
             if (!WFF && LONE && lone_on && --lcd == 0u) {
                 lcd = lone_on;
                 loneb = lone_mask();
@@ -1041,7 +1055,7 @@ sim_kernel(const SimArgs *Ap) {
                 const uint32_t endc = (uint32_t)live & (gidle | (uint32_t)((nd.ctl & C_ASSERT) != 0u) |
                                                         (uint32_t)(rounds >= thr) | (uint32_t)(nccv > ocap));
                 const uint64_t endb = __ballot(endc != 0u) | loneb;
-                if (endb == 0) return;
+                if ((SIM_RFL ? uni32((uint32_t)(endb != 0)) : (uint32_t)(endb != 0)) == 0u) return;
             } else {
                 /* a group field of actb | ~liveb that is zero: a live group with no active lane */
                 const uint64_t flagb = __ballot((nd.ctl & C_ASSERT) != 0u || rounds >= thr) |
@@ -1196,7 +1210,7 @@ sim_kernel(const SimArgs *Ap) {
                     }
                 }
             }
-            const uint64_t nlive = __ballot(live);
+            const uint64_t nlive = SIM_RFL ? uni64(__ballot(live)) : __ballot(live);
             /* budget pass: once a slot of this wave found no new system, the wave's remaining
              * systems get the late budget, so the launch's tail is not a system claimed last
              * running its full budget at falling occupancy (the resume pass continues them) */
@@ -1405,7 +1419,7 @@ ser_kernel(const SimArgs *Ap) {
      * budget pass, taken in suspension order), then the rest last-suspended first, as the
      * lock-step resume (their records the likeliest still in the MALL) */
     const uint32_t nlong = (SER_LONG && Ap->serfmt && Ap->susp_long) ? *Ap->susp_long : 0u;
-    const uint32_t n = *Ap->d_n + nlong;
+    const uint32_t n = SIM_RFL ? uni32(*Ap->d_n + nlong) : *Ap->d_n + nlong;   /* (sim_kernel's n) */
     const uint32_t lcap = Ap->susp_cap;
     const uint32_t *const list = Ap->list;
     /* global (not flat) accesses: a pending flat operation makes every later wait a full
@@ -2296,6 +2310,7 @@ static const char *build_variant() {
     add("SER_LONG", SER_LONG, 0);
     add("REC_PROBE", REC_PROBE, 0);
     add("SIM_UNI", SIM_UNI, 1);
+    add("SIM_RFL", SIM_RFL, 1);
     add("SIM_TAILPROBE", SIM_TAILPROBE, 0);
     add("TRAFFIC_PROBE", TRAFFIC_PROBE, 0);
     add("SER_PROBE", SER_PROBE, 0);

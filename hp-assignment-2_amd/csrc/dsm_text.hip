@@ -349,6 +349,9 @@ DEVI uint32_t lowmask(uint32_t n) { return n >= 32u ? 0xFFFFFFFFu : (1u << n) - 
 #ifndef PARSE_TRANSPOSE
 #define PARSE_TRANSPOSE 1   /* newline mask by one 4 x 8 bit transpose: 8.23-8.36 vs 8.91-8.96 ms */
 #endif
+#ifndef PARSE_UNI
+#define PARSE_UNI 1         /* wave index, and so the file loop, uniform (readfirstlane) */
+#endif
 #ifndef PARSE_PROBE
 #define PARSE_PROBE 0       /* timing probes of the FAST pass (results invalid): 1 no decode, 2 decode
                                without the store, 3 decode with the chunk words from registers */
@@ -360,7 +363,11 @@ parse_kernel(const uint8_t *text, const uint64_t *off, uint64_t n_files, uint32_
              uint32_t *flist, uint32_t *fcount) {
     constexpr uint32_t K = BPL / 16, WIN = 64 * BPL;
     __shared__ __attribute__((aligned(16))) uint8_t s_txt[PW][WIN + PHALO + 16];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    /* the wave index stated wave-uniform (v_readfirstlane): derived from threadIdx, the
+     * compiler's uniformity analysis takes it as lane-varying, and with it the file index,
+     * the window position and every loop over them (exec-masked loops, state in VGPRs) */
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = PARSE_UNI ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : threadIdx.x >> 6;
     uint8_t *const st = s_txt[wv];
     /* FAST: every file; EXACT: the files FAST abandoned (flist[0 .. *fcount)) */
     const uint64_t nf = FAST ? n_files : (uint64_t)*fcount;

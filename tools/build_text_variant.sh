@@ -8,6 +8,6 @@ T=$(mktemp -d)
 $H "$@" -Rpass-analysis=kernel-resource-usage -c hp-assignment-2_amd/csrc/dsm_text.hip -o "$T/t.o" 2>"$T/w.txt"
 grep -A10 "parse_kernelILj32E" "$T/w.txt" | grep -E "VGPRs|Occupancy|Spill" | head -4
 mkdir -p ab
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC hp-assignment-2_amd/build/dsm_engine.o "$T/t.o" hp-assignment-2_amd/build/dsm_host.o -o "ab/libdsm_$NAME.so"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC hp-assignment-2_amd/build/dsm_engine.o "$T/t.o" hp-assignment-2_amd/build/dsm_host.o hp-assignment-2_amd/build/dsm_group.o -L/opt/rocm/lib -lrccl -o "ab/libdsm_$NAME.so"
 rm -rf "$T"
 echo "ab/libdsm_$NAME.so"
