@@ -1050,7 +1050,17 @@ sim_kernel(const SimArgs *Ap) {
                  * with an assert, the round limit / budget or an overflowing inbox (C3 budget
                  * pass 24.5 -> 23.8 ms, C5 15.9 -> 15.5; in the kernel without suspend-on-lone,
                  * C4's, 17.3 -> 17.6: there the mask form below is kept) */
-                const uint32_t gidle = ((uint32_t)(actb >> gbase) & NPM) == 0u;
+                uint32_t gidle;
+                if constexpr (SIM_UNI == 2) {
+                    /* the groups with an active lane as a wave mask, each such group's field
+                     * all ones (scalar ops on the uniform actb), read per lane as a lane mask */
+                    constexpr uint64_t FTOP = NP == 8 ? 0x8080808080808080ull : 0x8888888888888888ull;
+                    constexpr uint64_t FLOW = ~FTOP;
+                    const uint64_t one = ((((actb & FLOW) + FLOW) | actb) & FTOP) >> (NP - 1);
+                    gidle = __builtin_amdgcn_inverse_ballot_w64((one << NP) - one) ? 0u : 1u;
+                } else {
+                    gidle = ((uint32_t)(actb >> gbase) & NPM) == 0u;
+                }
                 /* bitwise, not && / ||: short-circuit conditions are compiled into branches */
                 const uint32_t endc = (uint32_t)live & (gidle | (uint32_t)((nd.ctl & C_ASSERT) != 0u) |
                                                         (uint32_t)(rounds >= thr) | (uint32_t)(nccv > ocap));
