@@ -137,6 +137,11 @@ DEVI uint64_t uni64(uint64_t x) { return ((uint64_t)uni32((uint32_t)(x >> 32)) <
 #define SIM_RFL 1           /* the round loop's wave-uniform values (the live mask, the end test,
                                the lone-check countdown) pinned uniform with readfirstlane */
 #endif
+#ifndef SIM_R2
+#define SIM_R2 0            /* plain budget kernels: a third trace chunk in registers and the refill
+                               as one 32-B load every 16 instructions (half the chunk loads, each
+                               a line fetch: the scattered 16-B loads find no line in L2) */
+#endif
 #ifndef REC_PROBE
 #define REC_PROBE 0         /* probe build (hashes invalid): no node records and no digest pass, to
                                time what the records cost the step */
@@ -476,6 +481,8 @@ sim_kernel(const SimArgs *Ap) {
      * run only (M_SERB) */
     constexpr bool LONE = BUD && !FF && (MODE & M_SERB) != 0;
     constexpr bool UNI = SIM_UNI != 0 && LONE;     /* the per-round end test as one ballot */
+    /* paired refills (SIM_R2): the plain kernels, whose ip only ever moves by one issue */
+    constexpr bool R2 = SIM_R2 != 0 && BUD && !FF && !GEN;
     constexpr int SW = susp_words(RING);
     /* fast-forward probe interval: FF_PROBE iterations after a probe that found a group,
      * doubling up to FF_PROBE_MAX after each one that found none (workloads without hit
@@ -558,6 +565,9 @@ sim_kernel(const SimArgs *Ap) {
 
     Node nd;
     uint32_t cur[4] = {0, 0, 0, 0}, nxt[4] = {0, 0, 0, 0};
+    /* R2: chunk k + 2 while the chunk in cur (k = ip >> 3) is even; the refill consuming an
+     * odd chunk loads k + 2 and k + 3 together (one line fetch for both) */
+    uint32_t nx2[4] = {0, 0, 0, 0};
     /* FF: the line tags for a hit, a byte per line (RD needs a valid line, state != I; WR one
      * in M or E, state <= E; 0xFF never equals a 7-bit address), set at mode entry: in the
      * mode no message arrives and a write hit on E leaves M, still a hit for both */
@@ -596,6 +606,12 @@ sim_kernel(const SimArgs *Ap) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) { cur[k] = q[(7 + k) * NP]; nxt[k] = q[(11 + k) * NP]; }
             if (!GEN) tb = tslot();
+            if (R2 && ((nd.ip >> 3) & 1u) == 0u) {          /* the even phase needs k + 2 */
+                const uint32_t pc = (nd.ip & ~7u) + 16u;
+                const uint4 v2 = ld16(tb + (pc + 8u <= stride ? pc : stride - 8u));
+                nx2[0] = v2.x; nx2[1] = v2.y; nx2[2] = v2.z; nx2[3] = v2.w;
+                wait_vmcnt0();
+            }
             rmsg = s_ring[wv][nd.rh & 0xFFu][lane];          /* the head, as the loop keeps it */
             return;
         }
@@ -627,6 +643,10 @@ sim_kernel(const SimArgs *Ap) {
             const uint4 v0 = ld16(tb), v1 = ld16(tb + (stride > 8 ? 8 : 0));
             cur[0] = v0.x; cur[1] = v0.y; cur[2] = v0.z; cur[3] = v0.w;
             nxt[0] = v1.x; nxt[1] = v1.y; nxt[2] = v1.z; nxt[3] = v1.w;
+            if (R2) {
+                const uint4 v2 = ld16(tb + (stride > 16 ? 16 : stride - 8));
+                nx2[0] = v2.x; nx2[1] = v2.y; nx2[2] = v2.z; nx2[3] = v2.w;
+            }
             wait_vmcnt0();
         }
     };
@@ -893,8 +913,24 @@ sim_kernel(const SimArgs *Ap) {
              * HBM latency overlaps this round's transition and delivery (a load consumed in the
              * same basic block stalls the whole wave on HBM). */
             const bool refill = !GEN && doIssue && ((nd.ip + 1) & 7u) == 0 && nd.ip + 1 < nd.nins;
-            uint4 pf;
-            if (refill) pf = ld16(tb + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
+            uint4 pf, pf2;
+            if (R2 && SIM_R2 == 2) {
+                /* the rotation consuming an odd chunk loads the next two, 32 B in one line:
+                 * k + 2 straight into nx2 (dead in this phase), k + 3 into pf */
+                if (refill && ((nd.ip + 1) & 15u) == 0u) {
+                    const uint4 a2 = ld16(tb + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
+                    pf = ld16(tb + (nd.ip + 17 < stride ? nd.ip + 17 : stride - 8));
+                    nx2[0] = a2.x; nx2[1] = a2.y; nx2[2] = a2.z; nx2[3] = a2.w;
+                }
+            } else if (R2) {
+                /* the rotation consuming an odd chunk loads the next two, 32 B in one line */
+                if (refill && ((nd.ip + 1) & 15u) == 0u) {
+                    pf = ld16(tb + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
+                    pf2 = ld16(tb + (nd.ip + 17 < stride ? nd.ip + 17 : stride - 8));
+                }
+            } else if (refill) {
+                pf = ld16(tb + (nd.ip + 9 < stride ? nd.ip + 9 : stride - 8));
+            }
             const uint32_t headn = (head0 + 1 == (uint32_t)RING) ? 0u : head0 + 1;
             nd.rh = hasMsg ? (headn | ((cnt0 - 1) << 8)) : nd.rh;
             uint32_t w = rmsg;
@@ -1018,7 +1054,20 @@ sim_kernel(const SimArgs *Ap) {
                 rmsg = s_ring[wv][hh][lane];          /* next round's head, prefetched */
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            if (refill) {
+            if (R2 && SIM_R2 == 2 && refill) {
+                /* cur <- nxt <- nx2 always; after a pair load nx2 <- pf (k + 3) */
+    #pragma unroll
+                for (int k = 0; k < 4; ++k) { cur[k] = nxt[k]; nxt[k] = nx2[k]; }
+                if ((nd.ip & 15u) == 0u) { nx2[0] = pf.x; nx2[1] = pf.y; nx2[2] = pf.z; nx2[3] = pf.w; }
+            } else if (R2 && refill) {
+                /* ip is already past the issue: an even ip means an odd chunk was consumed */
+                const bool pair = (nd.ip & 15u) == 0u;
+    #pragma unroll
+                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+                nxt[0] = pair ? pf.x : nx2[0]; nxt[1] = pair ? pf.y : nx2[1];
+                nxt[2] = pair ? pf.z : nx2[2]; nxt[3] = pair ? pf.w : nx2[3];
+                if (pair) { nx2[0] = pf2.x; nx2[1] = pf2.y; nx2[2] = pf2.z; nx2[3] = pf2.w; }
+            } else if (refill) {
     #pragma unroll
                 for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
                 nxt[0] = pf.x; nxt[1] = pf.y; nxt[2] = pf.z; nxt[3] = pf.w;
@@ -2321,6 +2370,7 @@ static const char *build_variant() {
     add("REC_PROBE", REC_PROBE, 0);
     add("SIM_UNI", SIM_UNI, 1);
     add("SIM_RFL", SIM_RFL, 1);
+    add("SIM_R2", SIM_R2, 0);
     add("SIM_TAILPROBE", SIM_TAILPROBE, 0);
     add("TRAFFIC_PROBE", TRAFFIC_PROBE, 0);
     add("SER_PROBE", SER_PROBE, 0);
