@@ -1114,7 +1114,7 @@ sim_kernel(const SimArgs *Ap) {
                 const uint32_t endc = (uint32_t)live & (gidle | (uint32_t)((nd.ctl & C_ASSERT) != 0u) |
                                                         (uint32_t)(rounds >= thr) | (uint32_t)(nccv > ocap));
                 const uint64_t endb = __ballot(endc != 0u) | loneb;
-                if ((SIM_RFL ? uni32((uint32_t)(endb != 0)) : (uint32_t)(endb != 0)) == 0u) return;
+                if (endb == 0) return;
             } else {
                 /* a group field of actb | ~liveb that is zero: a live group with no active lane */
                 const uint64_t flagb = __ballot((nd.ctl & C_ASSERT) != 0u || rounds >= thr) |
