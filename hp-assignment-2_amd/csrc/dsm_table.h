@@ -352,6 +352,28 @@ DSM_HD void dt_decode(uint32_t w, uint32_t *a, uint32_t *v, uint32_t *excl, uint
     *a = (w >> 8) & 0x7Fu; *v = w & 0xFFu; *excl = (w >> 15) & 1u; *r2 = (w >> 20) & 7u; *s = (w >> 24) & 7u;
 }
 
+/* Three-input bitwise function (v_bitop3_b32 on gfx950): bit i of the result is bit
+ * (a_i << 2 | b_i << 1 | c_i) of the truth table tt (a = 0xF0, b = 0xCC, c = 0xAA: OR3 is 0xFE,
+ * (a & b) | c is 0xEA).  On gfx950 it issues at full rate with VGPR or inline-constant
+ * operands, where the v_or3_b32 / v_and_or_b32 the compiler picks for the same expressions
+ * issue at half rate (tools/calib/valu_rate.hip); the transition round is bound by its VALU
+ * issue, so the datapath's three-way combinations are stated with it (DT_B3). */
+#ifndef DT_B3
+#define DT_B3 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && DT_B3
+#define dt_b3(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))
+#else
+DSM_HD uint32_t dt_b3(uint32_t a, uint32_t b, uint32_t c, uint32_t tt) {
+    uint32_t r = 0;
+    for (uint32_t k = 0; k < 8; ++k)
+        if ((tt >> k) & 1u)
+            r |= ((k & 4u) ? a : ~a) & ((k & 2u) ? b : ~b) & ((k & 1u) ? c : ~c);
+    return r;
+}
+#endif
+#define DT_OR3 0xFEu
+
 /* bit-field extract; width 0 gives 0 (v_bfe_u32) */
 DSM_HD uint32_t dt_ubfe(uint32_t x, uint32_t lo, uint32_t w) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -377,8 +399,9 @@ DSM_HD uint32_t dt_index(const DtIn &in, uint32_t hdr, uint32_t *evDb_out) {
     const uint32_t home = (H == in.node), hit = (in.La == in.a);
     const uint32_t evDb = in.Db & ~(1u << in.s);
     const uint32_t rem = (uint32_t)__builtin_popcount(evDb & in.np_mask);    /* countSharers */
-    const uint32_t C = in.excl | (hit << 1) | (in.Ls << 2) | (home << 4) | ((uint32_t)(in.node == in.r2) << 5) |
-                       (in.Ds << 6) | (dt_ubfe(in.Db, in.s, 1) << 8) | ((rem < 2u ? rem : 2u) << 9);
+    const uint32_t C = dt_b3(dt_b3(in.excl, hit << 1, in.Ls << 2, DT_OR3),
+                             dt_b3(home << 4, (uint32_t)(in.node == in.r2) << 5, in.Ds << 6, DT_OR3),
+                             (dt_ubfe(in.Db, in.s, 1) << 8) | ((rem < 2u ? rem : 2u) << 9), DT_OR3);
     *evDb_out = evDb;
     return (hdr >> 16) + dt_ubfe(C, hdr & 31u, (hdr >> 5) & 7u);
 }
@@ -453,6 +476,7 @@ DSM_HD DtOut dt_apply_xy(const DtIn &in, uint32_t X, uint32_t Y, uint32_t W0, ui
     /* node control word (pending byte, wait bit 8, assert bit 11): ctl' = ctl & ~cclr | cset */
     const uint32_t pm = (W1 & W1_PEND) ? 0xFFu : 0u;
     o.cset = ((W1 >> 12) & (DT_CTL_WAIT | DT_CTL_ASSERT)) | (in.v & pm);   /* WSET, ASSERT */
+    /* (the kernel's ctl update, ctl & ~cclr | cset, is one v_bitop3 already) */
     o.cclr = ((W1 >> 13) & DT_CTL_WAIT) | pm;                                /* WCLR        */
     o.wset = (W1 & W1_WSET) != 0u;
     o.wclr = (W1 & W1_WCLR) != 0u;
