@@ -260,6 +260,9 @@ enum : uint32_t {
 #define W1_ASSERT (1u << 23)
 #define W1_DSEL(x) ((uint32_t)(x) << 24)   /* dir state: selector 1 keep, 4 + k state k      */
 #define W1_O1(x) ((uint32_t)(x) << 27)     /* second word: 0 none, 1 RREQ, 2 WREQ, 3 UPGRADE  */
+#define W1_BSEL(x) ((uint32_t)(x) << 29)   /* the dir bv base again, as a byte-permute selector
+                                            * over {0 (bytes 4-7), Y (bytes 0-3)}: 2 Db, 3 Db &
+                                            * ~sbit, 4 zero -- one v_perm_b32 (DT_BSEL)       */
 
 /* The 0xFF gates of dt_entry are resolved here.  A line leaves INVALID only by being filled
  * (line.address = a <= 0x7F), and line.address never returns to 0xFF, so a valid line never
@@ -281,6 +284,7 @@ static inline void dt_compile(uint32_t e, uint32_t h, uint32_t *w0, uint32_t *w1
     *w1 = W1_LSEL((e & E_LS) ? 4u + ((e >> 4) & 3u) : 0u) |
           W1_DSEL((e & E_DS) ? 4u + ((e >> 11) & 3u) : 1u) |
           W1_DBASE((e & E_DBANDS) ? 1u : (e & E_DBAND0) ? 2u : 0u) |
+          W1_BSEL((e & E_DBANDS) ? 3u : (e & E_DBAND0) ? 4u : 2u) |
           ((e & E_DBORS) ? W1_ORS : 0u) | ((e & E_DBORR) ? W1_ORR : 0u) |
           ((e & E_O0) ? W1_O0 : 0u) | W1_T((e >> 15) & 15u) | ((e & E_O0LA) ? W1_O0LA : 0u) |
           ((e & E_O0RS) ? W1_R2S : 0u) | ((e & E_O0RR) ? W1_R2R : 0u) | ((e & E_O0X) ? W1_X : 0u) |
@@ -373,6 +377,9 @@ DSM_HD uint32_t dt_b3(uint32_t a, uint32_t b, uint32_t c, uint32_t tt) {
 }
 #endif
 #define DT_OR3 0xFEu
+#ifndef DT_BSEL
+#define DT_BSEL 1
+#endif
 
 /* bit-field extract; width 0 gives 0 (v_bfe_u32) */
 DSM_HD uint32_t dt_ubfe(uint32_t x, uint32_t lo, uint32_t w) {
@@ -446,8 +453,14 @@ DSM_HD DtOut dt_apply_xy(const DtIn &in, uint32_t X, uint32_t Y, uint32_t W0, ui
     o.S = S;
     o.nLs = S & 0xFFu;
     o.nDs = S >> 24;
+#if DT_BSEL
+    /* the base byte picked from Y = {pend, Mv, Db, Db & ~sbit} by the entry's selector: one
+     * half-rate permute where the two-level select took two compares and two selects */
+    const uint32_t base = dt_perm(0u, Y, (W1 >> 29) | 0x0C0C0C00u);
+#else
     const uint32_t db = (W1 >> 5) & 3u;
     const uint32_t base = (db & 2u) ? 0u : (db ? (evDb & 0xFFu) : in.Db);
+#endif
     o.nDb = base | ((W1 & W1_ORS) ? sbit : 0u) | ((W1 & W1_ORR) ? (1u << in.r2) : 0u);
     /* first outgoing word: payload and address bytes by one permute of {P, X} (payload =
      * P byte 3; address = X byte 0 (a) or byte 2 (La), per W1_O0LA at selector bit 9),
